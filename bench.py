@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: GB/s of stream scanned (+ matches/sec) on
+snort.dict, one process per GPU (BASELINE.json configs 3 and 4).
+
+A "step" is one scan of the rank's whole stream shard (default 1 GiB of
+seeded synthetic ASCII, generated on the device, resident in HBM before the
+timed region) through the HIP kernel, writing the dense per-position match
+ids (u32; the read_block contract).  Shards are independent streams (one per
+rank, distinct seeds): weak scaling, no data-path collective.  The only
+collective is the RCCL all-reduce of match counts and the max-over-ranks
+time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints one JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "GB/s stream scanned + matches/sec, snort.dict, 1/2/4/8 MI355X vs CPU ref"
+DATA = os.path.join(REPO, "tests", "golden", "data")
+DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--dict", default="snort", choices=list(DICTS))
+    p.add_argument("--bytes", type=int, default=1 << 30, help="stream bytes per GPU")
+    p.add_argument("--mode", default="dense", choices=["dense", "count"])
+    p.add_argument("--kernel", default="rt", choices=["rt", "ac"])
+    p.add_argument("--stream", default="ascii", choices=["ascii", "bytes"])
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--cpu-sample", type=int, default=256 << 20, help="bytes of the CPU-baseline sample")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """The reference's own per-byte AC loop (oracle/_ref/ref_driver, built from
+    the reference's sources) on a bounded sample, 1 core; the C port of it
+    (oracle/ac_oracle.c) when that binary is absent.  Test infrastructure used
+    here only as the measured baseline."""
+    mode = 0 if args.stream == "ascii" else 1
+    paths = [os.path.join(DATA, d) for d in DICTS[args.dict]]
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_driver")
+    sample = f"first {args.cpu_sample} bytes of the seed-{args.seed} {args.stream} stream, {args.dict}.dict"
+    if os.path.exists(ref):
+        try:
+            r = subprocess.run([ref, "time", str(args.seed), str(mode), str(args.cpu_sample)] + paths,
+                               check=True, capture_output=True, text=True, timeout=600)
+            j = json.loads(r.stdout)
+            return {"value": round(j["MBps"] / 1000.0, 6), "unit": "GB/s", "cores": 1, "kind": "reference",
+                    "sample": sample + "; reference Core/src objects, mps_table[MPS_AC].read_char per byte",
+                    "seconds": j["seconds"], "nonnull": j["nonnull"]}
+        except (subprocess.SubprocessError, OSError, ValueError):
+            pass
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import patternmatching_amd as pm
+    from oracle_lib import Oracle
+    o = Oracle(paths)
+    secs, nonnull = o.time_scan(pm.gen_stream(args.cpu_sample, args.seed, mode), threads=1)
+    return {"value": round(args.cpu_sample / secs / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": sample + "; oracle/ac_oracle.c per-byte read_char", "seconds": secs, "nonnull": nonnull}
+
+
+def load_traffic(workload_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one
+    exists for this exact workload (profiles/traffic.json)."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f).get(workload_key)
+        return t
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    # CPU leg first, before this process touches the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args)
+
+    import torch
+    import torch.distributed as dist
+    import patternmatching_amd as pm
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    lib = pm.load()
+    lib.pm_hip_set_device(local)
+
+    d = pm.Dictionary([os.path.join(DATA, x) for x in DICTS[args.dict]])
+    m = pm.HipMatcher(args.kernel)
+    m.add_dictionary(d)
+    m.compile()
+
+    n = args.bytes
+    stream = torch.cuda.current_stream()
+    text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    seed = args.seed + rank  # independent shard per rank
+    if lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, seed, 0 if args.stream == "ascii" else 1,
+                                    stream.cuda_stream) != 0:
+        raise RuntimeError(lib.pm_hip_last_error().decode())
+    out = torch.empty(n, dtype=torch.int32, device="cuda") if args.mode == "dense" else None
+    count = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out_ptr = out.data_ptr() if out is not None else None
+
+    def step():
+        m.scan_device(text.data_ptr(), 0, 0, n, out_ptr, count.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    count.zero_()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        step()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+    matches = count.clone()
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(matches, op=dist.ReduceOp.SUM)  # RCCL over xGMI: the match-count reduction
+    elapsed, kernel_ms = stats.tolist()
+    total_matches = int(matches.item())
+
+    if rank == 0:
+        total_bytes = world * n * args.steps
+        value = total_bytes / elapsed / 1e9
+        alg_per_pos = 5 if args.mode == "dense" else 1  # 1 B read + 4 B id written (dense)
+        achieved = n * alg_per_pos / (kernel_ms * 1e-3) / 1e9
+        workload_key = f"{args.dict}-{args.stream}-{n}-{args.mode}-{args.kernel}"
+        traffic = load_traffic(workload_key)
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: seeded splitmix64 %s stream per GPU (DESIGN.md §5), generated in HBM; "
+                    "dictionaries from the reference" % args.stream,
+            "config": {
+                "workload": f"{args.dict}.dict, {n} B {args.stream} stream per GPU, "
+                            f"{'dense u32 match id per position' if args.mode == 'dense' else 'match count only'}",
+                "dict": args.dict,
+                "stream_bytes_per_gpu": n,
+                "mode": args.mode,
+                "kernel": {"rt": "reverse-suffix-trie walk", "ac": "Aho-Corasick dense DFA"}[args.kernel],
+                "parallelism": f"independent stream shards x{world}",
+            },
+            "matches_per_sec": round(total_matches / elapsed, 1),
+            "matches_per_step": total_matches // max(1, args.steps),
+            "kernel_ms": round(kernel_ms, 4),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": n * alg_per_pos,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

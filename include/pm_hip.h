@@ -1,0 +1,116 @@
+/*
+ * pm_hip.h -- C-ABI of the MI355X (gfx950) matcher library libpm.so.
+ *
+ * Two groups of entry points:
+ *
+ * 1. The plugin functions behind pm_mps_table (include/pm_mps.h).  Each one
+ *    replaces the reference function named beside it, with the same
+ *    argument meaning and the same "no error channel" behaviour: a HIP
+ *    failure prints a message and exits(1), like FatalExit()
+ *    (/root/reference/Core/src/util.h:37-39).
+ *
+ *      reference (Core/src/)            this library
+ *      mpac.c:236  ac_create            pm_hip_rt_create / pm_hip_ac_create
+ *      mpac.c:257  ac_add_pattern       pm_hip_add_pattern
+ *      mpac.c:282  ac_compile           pm_hip_compile
+ *      mpac.c:304  ac_read_char         pm_hip_read_char
+ *      (none)                           pm_hip_read_block (batched read_char)
+ *      mpac.c:328  ac_total_mem         pm_hip_total_mem
+ *      mpac.c:339  ac_reset             pm_hip_reset
+ *      mpac.c:349  ac_free              pm_hip_free
+ *      mpac.c:358  mps_ac_register      pm_mps_hip_rt_register / pm_mps_hip_ac_register
+ *
+ *    The same functions serve both algorithms; the object created decides
+ *    which kernel runs.
+ *
+ * 2. Device-resident batch entry points for callers that keep the stream in
+ *    HBM (bench.py, the multi-GPU driver).  They return 0 on success and a
+ *    negative code on failure (message via pm_hip_last_error()).
+ *
+ * Pattern ids inside the library are "gids": 1..n_patterns, 0 = no match.
+ * pm_hip_gid_index maps a gid back to the 0-based add_pattern call order.
+ */
+#ifndef PM_HIP_H
+#define PM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "pm_mps.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- 1. plugin ABI (MpsElem members) ---------------------------------- */
+void* pm_hip_rt_create(void);
+void* pm_hip_ac_create(void);
+void pm_hip_add_pattern(void* obj, char* pat, size_t len, pm_pattern_id_t id);
+void pm_hip_compile(void* obj);
+pm_pattern_id_t pm_hip_read_char(void* obj, char c);
+void pm_hip_read_block(void* obj, const char* buf, size_t n, pm_pattern_id_t* out);
+size_t pm_hip_total_mem(void* obj);
+void pm_hip_reset(void* obj);
+void pm_hip_free(void* obj);
+
+void pm_mps_hip_rt_register(PmMpsElem* slot);
+void pm_mps_hip_ac_register(PmMpsElem* slot);
+
+/* ---- 2. batch / introspection ----------------------------------------- */
+
+/* Same as pm_hip_read_block but writes gids (u32, 0 = none) instead of
+ * pattern ids; state carries across calls exactly like read_block. */
+int pm_hip_read_block_gid(void* obj, const uint8_t* buf, size_t n, uint32_t* out_gid);
+
+/*
+ * Scan positions [pos0, pos0+n) of the device buffer d_text.
+ *   stream_start  index in d_text of the stream's first byte (<= pos0);
+ *                 bytes in [stream_start, pos0) are context: they are looked
+ *                 back at but produce no output.  Context of
+ *                 pm_hip_max_pattern_len()-1 bytes makes the result exact for
+ *                 a position anywhere in a longer stream.
+ *   pos0          must be a multiple of 16; d_text 16-byte aligned and
+ *                 readable up to round_up(pos0+n, 16).
+ *   d_out         n u32 gids (16-byte aligned), or NULL for count-only.
+ *   d_count       device u64, incremented by the number of non-null
+ *                 positions (may be NULL).
+ *   hip_stream    hipStream_t to launch on (NULL = default stream).
+ * Asynchronous: returns after the launch.
+ */
+int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0,
+                       int64_t n, uint32_t* d_out, unsigned long long* d_count, void* hip_stream);
+
+/* Device-side synthetic stream, identical to pm_gen_stream_host(). */
+int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
+                             void* hip_stream);
+void pm_gen_stream_host(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode);
+
+uint32_t pm_hip_n_patterns(void* obj);
+uint32_t pm_hip_max_pattern_len(void* obj);
+/* gid (1..n) -> 0-based add_pattern order; returns UINT32_MAX if out of range */
+uint32_t pm_hip_gid_index(void* obj, uint32_t gid);
+/* Which kernel a compiled object runs: 1 = reverse trie, 2 = AC DFA. */
+int pm_hip_kernel_kind(void* obj);
+/* Seconds of device time of the scan kernels issued through read_block
+ * since the last reset (hipEvent based). */
+double pm_hip_device_seconds(void* obj);
+/* Bytes of flattened tables per kind, for DESIGN/bench reporting. */
+size_t pm_hip_table_bytes(void* obj);
+const char* pm_hip_last_error(void);
+/* Returns the number of HIP devices (0 when none); never exits. */
+int pm_hip_device_count(void);
+/* hipSetDevice for C callers (the CLI's -g); 0 on success. */
+int pm_hip_set_device(int device);
+
+/* ---- 3. host-only table images (no device; used by the CPU test suite
+ *         to check the flattener, and by DESIGN.md sizing) ------------ */
+/* kind 1 = reverse-trie image, 2 = AC dense-DFA image */
+void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int kind);
+int pm_flat_fits(void* handle);
+/* name: "t12" "t3" "b2" "rec" "next" "out" "index_of_gid"; returns element count */
+size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* elem_size);
+void pm_flat_free(void* handle);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PM_HIP_H */

@@ -1,0 +1,200 @@
+// pm_flatten.cpp -- see pm_flatten.h.
+#include "pm_flatten.h"
+
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+
+namespace {
+
+// A byte trie in BFS order: node 0 is the root, the children of a node are
+// contiguous ids [cstart, cstart+ccount) sorted by edge byte, and all nodes
+// of depth d precede all nodes of depth d+1.
+struct BfsTrie {
+    uint32_t n = 0;
+    std::vector<uint32_t> cstart, ccount, parent, gid, depth;
+    std::vector<uint8_t> label;  // edge byte from the parent
+
+    uint32_t child(uint32_t v, uint32_t c) const {
+        uint32_t lo = cstart[v], hi = lo + ccount[v];
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (label[mid] < c) lo = mid + 1;
+            else hi = mid;
+        }
+        return (lo < cstart[v] + ccount[v] && label[lo] == c) ? lo : 0;
+    }
+};
+
+BfsTrie build_trie(const std::vector<std::string>& pats, const PmGidMap& g, bool reversed) {
+    // creation-order trie with a hash map of edges
+    std::unordered_map<uint64_t, uint32_t> edge;
+    size_t total = 0;
+    for (const auto& p : pats) total += p.size();
+    edge.reserve(total + 16);
+    std::vector<uint32_t> gid(1, 0);
+    uint32_t n = 1;
+    for (size_t k = 0; k < pats.size(); ++k) {
+        const std::string& p = pats[k];
+        uint32_t cur = 0;
+        for (size_t t = 0; t < p.size(); ++t) {
+            uint8_t c = (uint8_t)(reversed ? p[p.size() - 1 - t] : p[t]);
+            uint64_t key = ((uint64_t)cur << 8) | c;
+            auto it = edge.find(key);
+            if (it == edge.end()) {
+                edge.emplace(key, n);
+                gid.push_back(0);
+                cur = n++;
+            } else {
+                cur = it->second;
+            }
+        }
+        if (!p.empty() && gid[cur] == 0) gid[cur] = g.gid_of_index[k];
+    }
+    // children lists by creation id, sorted by byte
+    std::vector<uint64_t> kids;  // (parent << 40) | (byte << 32) | child
+    kids.reserve(edge.size());
+    for (const auto& e : edge) kids.push_back(((e.first >> 8) << 40) | ((e.first & 0xFF) << 32) | e.second);
+    std::sort(kids.begin(), kids.end());
+    std::vector<uint32_t> kstart(n + 1, 0);
+    for (uint64_t x : kids) kstart[(x >> 40) + 1]++;
+    for (uint32_t v = 0; v < n; ++v) kstart[v + 1] += kstart[v];
+    // BFS renumbering
+    BfsTrie t;
+    t.n = n;
+    t.cstart.assign(n, 0);
+    t.ccount.assign(n, 0);
+    t.parent.assign(n, 0);
+    t.gid.assign(n, 0);
+    t.depth.assign(n, 0);
+    t.label.assign(n, 0);
+    std::vector<uint32_t> order;  // BFS id -> creation id
+    order.reserve(n);
+    order.push_back(0);
+    for (size_t h = 0; h < order.size(); ++h) {
+        uint32_t old = order[h];
+        uint32_t v = (uint32_t)h;
+        t.gid[v] = gid[old];
+        t.cstart[v] = (uint32_t)order.size();
+        t.ccount[v] = kstart[old + 1] - kstart[old];
+        for (uint32_t k = kstart[old]; k < kstart[old + 1]; ++k) {
+            uint32_t nv = (uint32_t)order.size();
+            t.parent[nv] = v;
+            t.label[nv] = (uint8_t)((kids[k] >> 32) & 0xFF);
+            t.depth[nv] = t.depth[v] + 1;
+            order.push_back((uint32_t)(kids[k] & 0xFFFFFFFFu));
+        }
+    }
+    return t;
+}
+
+}  // namespace
+
+PmGidMap pm_assign_gids(const std::vector<std::string>& pats) {
+    PmGidMap g;
+    const size_t P = pats.size();
+    g.gid_of_index.assign(P, 0);
+    g.index_of_gid.assign(1, 0);
+    g.index_of_gid.reserve(P + 1);
+    for (int pass = 0; pass < 2; ++pass)
+        for (size_t k = 0; k < P; ++k) {
+            bool short_pat = pats[k].size() <= 2;
+            if ((pass == 0) == short_pat) {
+                g.gid_of_index[k] = (uint32_t)g.index_of_gid.size();
+                g.index_of_gid.push_back((uint32_t)k);
+            }
+        }
+    return g;
+}
+
+RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
+    RtImage im;
+    BfsTrie t = build_trie(pats, g, /*reversed=*/true);
+    im.nodes = t.n;
+    // best pattern on the path root..v (deepest pattern node, inclusive)
+    std::vector<uint32_t> best(t.n, 0);
+    for (uint32_t v = 1; v < t.n; ++v) best[v] = t.gid[v] ? t.gid[v] : best[t.parent[v]];
+
+    uint32_t n_short = 0;
+    for (const auto& p : pats) n_short += p.size() <= 2;
+    // depth-2 internal nodes, in BFS order, and the first depth-3 node
+    std::vector<uint32_t> n2i(t.n, UINT32_MAX);
+    uint32_t first_d3 = t.n;
+    for (uint32_t v = 1; v < t.n; ++v) {
+        if (t.depth[v] == 2 && t.ccount[v]) n2i[v] = im.n2int++;
+        if (t.depth[v] >= 3 && first_d3 == t.n) first_d3 = v;
+    }
+    im.nrec = t.n - first_d3;
+    im.fits = n_short < RT_CONT16 && im.n2int < RT_CONT16 && im.nrec < RT_CONT32;
+    if (!im.fits) return im;
+
+    im.t12.assign(RT_T1_BASE + 256, 0);
+    for (uint32_t c0 = 0; c0 < 256; ++c0) {
+        uint32_t n1 = t.child(0, c0);
+        im.t12[RT_T1_BASE + c0] = (uint16_t)(n1 ? best[n1] : 0);
+        for (uint32_t c1 = 0; c1 < 256; ++c1) {
+            uint32_t v = 0;
+            if (n1) {
+                uint32_t n2 = t.child(n1, c1);
+                if (!n2) v = best[n1];
+                else if (t.ccount[n2]) v = RT_CONT16 | n2i[n2];
+                else v = best[n2];
+            }
+            im.t12[(c0 << 8) | c1] = (uint16_t)v;
+        }
+    }
+    im.t3.assign((size_t)im.n2int * 256, 0);
+    im.b2.assign(im.n2int, 0);
+    for (uint32_t v = 1; v < t.n && t.depth[v] <= 2; ++v) {
+        if (n2i[v] == UINT32_MAX) continue;
+        uint32_t row = n2i[v];
+        im.b2[row] = best[v];
+        for (uint32_t c = 0; c < 256; ++c) im.t3[(size_t)row * 256 + c] = best[v];
+        for (uint32_t k = 0; k < t.ccount[v]; ++k) {
+            uint32_t n3 = t.cstart[v] + k;
+            im.t3[(size_t)row * 256 + t.label[n3]] = t.ccount[n3] ? (RT_CONT32 | (n3 - first_d3)) : best[n3];
+        }
+    }
+    im.rec.assign((size_t)im.nrec * RT_REC_WORDS, 0);
+    for (uint32_t v = first_d3; v < t.n; ++v) {
+        uint32_t* R = &im.rec[(size_t)(v - first_d3) * RT_REC_WORDS];
+        for (uint32_t k = 0; k < t.ccount[v]; ++k) {
+            uint32_t c = t.label[t.cstart[v] + k];
+            R[c >> 5] |= 1u << (c & 31);
+        }
+        R[8] = t.ccount[v] ? t.cstart[v] - first_d3 : 0;
+        R[9] = best[v];
+        uint32_t pre = 0;
+        for (int w = 0; w < 8; ++w) {
+            R[10 + (w >> 2)] |= pre << (8 * (w & 3));
+            pre += (uint32_t)__builtin_popcount(R[w]);
+        }
+    }
+    return im;
+}
+
+DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
+    DfaImage im;
+    BfsTrie t = build_trie(pats, g, /*reversed=*/false);
+    const uint32_t S = t.n;
+    im.states = S;
+    im.next.assign((size_t)S * 256, 0);
+    im.out.assign(S, 0);
+    std::vector<uint32_t> fail(S, 0);
+    // BFS order guarantees fail[v] (shallower) has its row before v's.
+    for (uint32_t v = 0; v < S; ++v) {
+        uint32_t* row = &im.next[(size_t)v * 256];
+        if (v) std::memcpy(row, &im.next[(size_t)fail[v] * 256], 256 * sizeof(uint32_t));
+        for (uint32_t k = 0; k < t.ccount[v]; ++k) {
+            uint32_t u = t.cstart[v] + k;
+            uint32_t c = t.label[u];
+            // failure of a child (mpac.c:172-180): the root's children fail to
+            // the root; otherwise follow v's failure with the same byte.
+            fail[u] = v ? im.next[(size_t)fail[v] * 256 + c] : 0;
+            row[c] = u;
+        }
+        // suffix link / output (mpac.c:179, :318)
+        im.out[v] = v == 0 ? 0 : (t.gid[v] ? t.gid[v] : im.out[fail[v]]);
+    }
+    return im;
+}

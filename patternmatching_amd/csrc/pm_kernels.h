@@ -1,0 +1,25 @@
+// pm_kernels.h -- launchers of the gfx950 scan kernels (pm_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+struct RtDev {
+    const uint16_t* t12;  // 65536 + 256 u16, staged into LDS per workgroup
+    const uint32_t* t3;   // n2int * 256
+    const uint32_t* b2;   // n2int
+    const uint32_t* rec;  // nrec * 12
+};
+
+struct DfaDev {
+    const uint32_t* next;  // states * 256
+    const uint32_t* out;   // states
+    int64_t warm;          // max pattern length - 1
+};
+
+// Positions [pos0, pos0+n) of text; bytes back to stream_start are context.
+// pos0 % 16 == 0; out (n u32) may be null; count (u64) may be null.
+hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
+                        unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s);
+hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
+                         unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s);
+hipError_t pm_launch_gen(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode, hipStream_t s);

@@ -1,0 +1,388 @@
+// pm_plugin.hip -- the GPU matcher objects behind the plugin ABI
+// (include/pm_hip.h, include/pm_mps.h).
+//
+// Object life cycle = the reference's (Core/src/mps.h:29-69):
+// create -> add_pattern x P (bytes borrowed: copied here) -> compile (flatten
+// + upload to HBM) -> per stream file: reset, then read_char / read_block
+// with state carried across calls -> total_mem -> free.
+//
+// The carried state is not an automaton state: for the reverse-trie kernel
+// it is the last max_len-1 stream bytes (every position only looks back
+// that far), and the DFA kernel re-derives its state from the same bytes
+// (warm-up).  read_block therefore stages [history | new bytes] in device
+// memory and scans the new positions with the history as context.
+//
+// Errors: the ABI has no error channel; every HIP failure prints and exits
+// (util.h:37-39 FatalExit semantics).  There is no CPU fallback: without a
+// HIP device, create() fails loudly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pm_flatten.h"
+#include "pm_hip.h"
+#include "pm_kernels.h"
+#include "pm_streamgen.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+[[noreturn]] void fatal(const char* what, hipError_t e) {
+    std::fprintf(stderr, "pm_hip: %s failed: %s\n", what, hipGetErrorString(e));
+    std::fflush(stderr);
+    std::exit(EXIT_FAILURE);
+}
+
+#define PM_CHECK(call)                            \
+    do {                                          \
+        hipError_t e_ = (call);                   \
+        if (e_ != hipSuccess) fatal(#call, e_);   \
+    } while (0)
+
+enum Kind { KIND_RT = 1, KIND_AC = 2 };
+
+constexpr size_t STAGE_POSITIONS = (size_t)64 << 20;  // read_block piece
+
+struct PmHip {
+    int kind_req = KIND_RT;
+    int kind = 0;
+    int device = 0;
+    int num_cu = 0;
+    bool compiled = false;
+    std::vector<std::string> pats;
+    std::vector<pm_pattern_id_t> ids;
+    uint32_t max_len = 0;
+    PmGidMap gids;
+    // device tables
+    RtDev rt{};
+    DfaDev dfa{};
+    std::vector<void*> allocs;
+    size_t table_bytes = 0;
+    // streaming
+    std::vector<uint8_t> hist;
+    uint8_t* d_stage = nullptr;
+    uint32_t* d_res = nullptr;
+    uint8_t* h_stage = nullptr;
+    uint32_t* h_res = nullptr;
+    size_t stage_cap = 0;  // positions
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double dev_seconds = 0.0;
+};
+
+void* dalloc_copy(PmHip* o, const void* src, size_t bytes) {
+    void* p = nullptr;
+    PM_CHECK(hipMalloc(&p, bytes ? bytes : 16));
+    if (bytes) PM_CHECK(hipMemcpy(p, src, bytes, hipMemcpyHostToDevice));
+    o->allocs.push_back(p);
+    o->table_bytes += bytes;
+    return p;
+}
+
+PmHip* create(int kind) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        std::fprintf(stderr, "pm_hip: no HIP device; this matcher has no CPU fallback\n");
+        std::exit(EXIT_FAILURE);
+    }
+    PmHip* o = new PmHip();
+    o->kind_req = kind;
+    PM_CHECK(hipGetDevice(&o->device));
+    hipDeviceProp_t prop;
+    PM_CHECK(hipGetDeviceProperties(&prop, o->device));
+    o->num_cu = prop.multiProcessorCount;
+    return o;
+}
+
+void ensure_stage(PmHip* o, size_t positions) {
+    if (positions <= o->stage_cap) return;
+    if (o->d_stage) {
+        PM_CHECK(hipFree(o->d_stage));
+        PM_CHECK(hipFree(o->d_res));
+        PM_CHECK(hipHostFree(o->h_stage));
+        PM_CHECK(hipHostFree(o->h_res));
+    }
+    size_t cap = std::max(positions, (size_t)1 << 16);
+    size_t stage_bytes = cap + o->max_len + 64;
+    PM_CHECK(hipMalloc(&o->d_stage, stage_bytes));
+    PM_CHECK(hipMalloc(&o->d_res, cap * sizeof(uint32_t)));
+    PM_CHECK(hipHostMalloc(&o->h_stage, stage_bytes, hipHostMallocDefault));
+    PM_CHECK(hipHostMalloc(&o->h_res, cap * sizeof(uint32_t), hipHostMallocDefault));
+    o->stage_cap = cap;
+}
+
+hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
+                  unsigned long long* count, hipStream_t s) {
+    if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, count, o->rt, o->num_cu, s);
+    return pm_launch_dfa(text, stream_start, pos0, n, out, count, o->dfa, o->num_cu, s);
+}
+
+// Scan n new bytes after the carried history; gids to out_gid.
+void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid) {
+    if (!o->compiled) {
+        std::fprintf(stderr, "pm_hip: read before compile\n");
+        std::exit(EXIT_FAILURE);
+    }
+    PM_CHECK(hipSetDevice(o->device));
+    const size_t keep = o->max_len ? o->max_len - 1 : 0;
+    size_t done = 0;
+    while (done < n) {
+        const size_t m = std::min(STAGE_POSITIONS, n - done);
+        ensure_stage(o, m);
+        const size_t h = o->hist.size();
+        const size_t ctx = (h + 15) & ~(size_t)15;  // new bytes start 16-aligned
+        std::memcpy(o->h_stage + ctx - h, o->hist.data(), h);
+        std::memcpy(o->h_stage + ctx, buf + done, m);
+        std::memset(o->h_stage + ctx + m, 0, 16);
+        PM_CHECK(hipMemcpyAsync(o->d_stage, o->h_stage, ctx + m + 16, hipMemcpyHostToDevice, o->stream));
+        PM_CHECK(hipEventRecord(o->ev0, o->stream));
+        PM_CHECK(launch(o, o->d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, o->d_res, nullptr, o->stream));
+        PM_CHECK(hipEventRecord(o->ev1, o->stream));
+        PM_CHECK(hipMemcpyAsync(o->h_res, o->d_res, m * sizeof(uint32_t), hipMemcpyDeviceToHost, o->stream));
+        PM_CHECK(hipStreamSynchronize(o->stream));
+        float ms = 0.f;
+        PM_CHECK(hipEventElapsedTime(&ms, o->ev0, o->ev1));
+        o->dev_seconds += ms * 1e-3;
+        std::memcpy(out_gid + done, o->h_res, m * sizeof(uint32_t));
+        // carry the last `keep` bytes of the stream
+        if (keep) {
+            if (m >= keep) {
+                o->hist.assign(buf + done + m - keep, buf + done + m);
+            } else {
+                o->hist.insert(o->hist.end(), buf + done, buf + done + m);
+                if (o->hist.size() > keep) o->hist.erase(o->hist.begin(), o->hist.end() - keep);
+            }
+        }
+        done += m;
+    }
+}
+
+PmHip* as(void* obj) { return static_cast<PmHip*>(obj); }
+
+}  // namespace
+
+extern "C" {
+
+int pm_hip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int pm_hip_set_device(int dev) { return hipSetDevice(dev) == hipSuccess ? 0 : -1; }
+
+const char* pm_hip_last_error(void) { return g_err; }
+
+void* pm_hip_rt_create(void) { return create(KIND_RT); }
+void* pm_hip_ac_create(void) { return create(KIND_AC); }
+
+void pm_hip_add_pattern(void* obj, char* pat, size_t len, pm_pattern_id_t id) {
+    PmHip* o = as(obj);
+    if (o->compiled) {
+        std::fprintf(stderr, "pm_hip: add_pattern after compile\n");
+        std::exit(EXIT_FAILURE);
+    }
+    if (len == 0) return;
+    o->pats.emplace_back(pat, len);  // borrowed bytes (PatternsTree.c:393-400): copy
+    o->ids.push_back(id);
+    o->max_len = std::max(o->max_len, (uint32_t)len);
+}
+
+void pm_hip_compile(void* obj) {
+    PmHip* o = as(obj);
+    PM_CHECK(hipSetDevice(o->device));
+    o->gids = pm_assign_gids(o->pats);
+    o->kind = o->kind_req;
+    if (o->kind == KIND_RT) {
+        RtImage im = pm_build_rt(o->pats, o->gids);
+        if (im.fits) {
+            o->rt.t12 = (const uint16_t*)dalloc_copy(o, im.t12.data(), im.t12.size() * 2);
+            o->rt.t3 = (const uint32_t*)dalloc_copy(o, im.t3.data(), im.t3.size() * 4);
+            o->rt.b2 = (const uint32_t*)dalloc_copy(o, im.b2.data(), im.b2.size() * 4);
+            o->rt.rec = (const uint32_t*)dalloc_copy(o, im.rec.data(), im.rec.size() * 4);
+        } else {
+            std::fprintf(stderr, "pm_hip: dictionary exceeds the reverse-trie u16 encoding; using the DFA kernel\n");
+            o->kind = KIND_AC;
+        }
+    }
+    if (o->kind == KIND_AC) {
+        DfaImage im = pm_build_dfa(o->pats, o->gids);
+        o->dfa.next = (const uint32_t*)dalloc_copy(o, im.next.data(), im.next.size() * 4);
+        o->dfa.out = (const uint32_t*)dalloc_copy(o, im.out.data(), im.out.size() * 4);
+        o->dfa.warm = o->max_len ? (int64_t)o->max_len - 1 : 0;
+    }
+    PM_CHECK(hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking));
+    PM_CHECK(hipEventCreate(&o->ev0));
+    PM_CHECK(hipEventCreate(&o->ev1));
+    o->compiled = true;
+}
+
+int pm_hip_read_block_gid(void* obj, const uint8_t* buf, size_t n, uint32_t* out_gid) {
+    scan_host(as(obj), buf, n, out_gid);
+    return 0;
+}
+
+void pm_hip_read_block(void* obj, const char* buf, size_t n, pm_pattern_id_t* out) {
+    PmHip* o = as(obj);
+    std::vector<uint32_t> g(std::min(n, STAGE_POSITIONS));
+    size_t done = 0;
+    while (done < n) {
+        size_t m = std::min(n - done, g.size());
+        scan_host(o, reinterpret_cast<const uint8_t*>(buf) + done, m, g.data());
+        for (size_t j = 0; j < m; ++j)
+            out[done + j] = g[j] ? o->ids[o->gids.index_of_gid[g[j]]] : PM_NULL_PATTERN_ID;
+        done += m;
+    }
+}
+
+// The per-byte entry point of the reference ABI.  It runs the same GPU scan
+// on one byte (correct, but one launch per byte): stream drivers use
+// read_block.
+pm_pattern_id_t pm_hip_read_char(void* obj, char c) {
+    pm_pattern_id_t r;
+    pm_hip_read_block(obj, &c, 1, &r);
+    return r;
+}
+
+size_t pm_hip_total_mem(void* obj) {
+    PmHip* o = as(obj);
+    return sizeof(PmHip) + o->table_bytes;
+}
+
+void pm_hip_reset(void* obj) {
+    PmHip* o = as(obj);
+    o->hist.clear();
+    o->dev_seconds = 0.0;
+}
+
+void pm_hip_free(void* obj) {
+    PmHip* o = as(obj);
+    (void)hipSetDevice(o->device);
+    for (void* p : o->allocs) (void)hipFree(p);
+    if (o->d_stage) {
+        (void)hipFree(o->d_stage);
+        (void)hipFree(o->d_res);
+        (void)hipHostFree(o->h_stage);
+        (void)hipHostFree(o->h_res);
+    }
+    if (o->ev0) (void)hipEventDestroy(o->ev0);
+    if (o->ev1) (void)hipEventDestroy(o->ev1);
+    if (o->stream) (void)hipStreamDestroy(o->stream);
+    delete o;
+}
+
+static void fill_slot(PmMpsElem* slot, const char* name, void* (*create_fn)(void)) {
+    slot->name = const_cast<char*>(name);
+    slot->create = create_fn;
+    slot->add_pattern = pm_hip_add_pattern;
+    slot->compile = pm_hip_compile;
+    slot->read_char = pm_hip_read_char;
+    slot->total_mem = pm_hip_total_mem;
+    slot->reset = pm_hip_reset;
+    slot->free = pm_hip_free;
+    slot->read_block = pm_hip_read_block;
+}
+
+void pm_mps_hip_rt_register(PmMpsElem* slot) { fill_slot(slot, "HIP Reverse-Trie", pm_hip_rt_create); }
+void pm_mps_hip_ac_register(PmMpsElem* slot) { fill_slot(slot, "HIP Aho-Corasick DFA", pm_hip_ac_create); }
+
+int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0, int64_t n,
+                       uint32_t* d_out, unsigned long long* d_count, void* hip_stream) {
+    PmHip* o = as(obj);
+    if (!o->compiled) { std::snprintf(g_err, sizeof(g_err), "not compiled"); return -1; }
+    if (pos0 % 16 || stream_start > pos0 || stream_start < 0 || n < 0 || ((uintptr_t)d_text & 15) ||
+        ((uintptr_t)d_out & 15)) {
+        std::snprintf(g_err, sizeof(g_err), "bad arguments (pos0 %% 16, stream_start <= pos0, 16-B alignment)");
+        return -2;
+    }
+    hipError_t e = hipSetDevice(o->device);
+    if (e == hipSuccess) e = launch(o, d_text, stream_start, pos0, n, d_out, d_count, (hipStream_t)hip_stream);
+    if (e != hipSuccess) {
+        std::snprintf(g_err, sizeof(g_err), "launch: %s", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
+}
+
+int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
+                             void* hip_stream) {
+    hipError_t e = pm_launch_gen(d_dst, offset, n, seed, mode, (hipStream_t)hip_stream);
+    if (e != hipSuccess) {
+        std::snprintf(g_err, sizeof(g_err), "gen: %s", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
+}
+
+void pm_gen_stream_host(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode) {
+    for (uint64_t k = 0; k < n; ++k) dst[k] = pm_stream_byte(offset + k, seed, mode);
+}
+
+uint32_t pm_hip_n_patterns(void* obj) { return (uint32_t)as(obj)->pats.size(); }
+uint32_t pm_hip_max_pattern_len(void* obj) { return as(obj)->max_len; }
+uint32_t pm_hip_gid_index(void* obj, uint32_t gid) {
+    PmHip* o = as(obj);
+    if (gid == 0 || gid >= o->gids.index_of_gid.size()) return UINT32_MAX;
+    return o->gids.index_of_gid[gid];
+}
+int pm_hip_kernel_kind(void* obj) { return as(obj)->kind; }
+double pm_hip_device_seconds(void* obj) { return as(obj)->dev_seconds; }
+size_t pm_hip_table_bytes(void* obj) { return as(obj)->table_bytes; }
+
+}  // extern "C"
+
+// ---- host-only table export (tests validate the flattened images on CPU) --
+namespace {
+struct PmFlatHandle {
+    PmGidMap g;
+    RtImage rt;
+    DfaImage dfa;
+    int kind = 0;
+};
+}  // namespace
+
+extern "C" {
+
+void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int kind) {
+    std::vector<std::string> v;
+    v.reserve(n);
+    for (size_t i = 0; i < n; ++i) v.emplace_back(pats[i], lens[i]);
+    PmFlatHandle* h = new PmFlatHandle();
+    h->kind = kind;
+    h->g = pm_assign_gids(v);
+    if (kind == KIND_RT) h->rt = pm_build_rt(v, h->g);
+    else h->dfa = pm_build_dfa(v, h->g);
+    return h;
+}
+
+int pm_flat_fits(void* handle) { return static_cast<PmFlatHandle*>(handle)->rt.fits ? 1 : 0; }
+
+size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* elem_size) {
+    PmFlatHandle* h = static_cast<PmFlatHandle*>(handle);
+    auto ret = [&](const auto& vec) {
+        *data = vec.data();
+        *elem_size = sizeof(vec[0]);
+        return vec.size();
+    };
+    std::string s(name);
+    if (s == "t12") return ret(h->rt.t12);
+    if (s == "t3") return ret(h->rt.t3);
+    if (s == "b2") return ret(h->rt.b2);
+    if (s == "rec") return ret(h->rt.rec);
+    if (s == "next") return ret(h->dfa.next);
+    if (s == "out") return ret(h->dfa.out);
+    if (s == "index_of_gid") return ret(h->g.index_of_gid);
+    *data = nullptr;
+    *elem_size = 0;
+    return 0;
+}
+
+void pm_flat_free(void* handle) { delete static_cast<PmFlatHandle*>(handle); }
+
+}  // extern "C"

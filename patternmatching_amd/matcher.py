@@ -1,0 +1,198 @@
+"""Python mirror of the plugin interface (include/pm_mps.h) over libpm.so.
+
+Names and argument meaning follow the reference's MpsElem
+(Core/src/mps.h:71-80) so tests read like the reference's own call order:
+
+    d = Dictionary(["et.dict"])              # PatternsTree.c:260-312
+    m = HipMatcher("rt")                     # mps_table[...].create()
+    m.add_dictionary(d)                      # add_pattern per unique pattern
+    m.compile()                              # flatten + upload to HBM
+    codes = m.read_block_codes(stream_bytes) # == read_char per byte
+    m.reset()                                # new stream file
+
+Every scan goes through the HIP kernels; without a GPU, ``HipMatcher``
+creation fails (the library exits, as the reference's FatalExit would).
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import load, PmPattern
+
+KIND_RT = 1
+KIND_AC = 2
+
+
+def parse_line(line: bytes):
+    """parser.c:63-99 via the library.  Returns the pattern bytes, or None
+    when the line is rejected or empty."""
+    lib = load()
+    n = len(line)
+    src = (ctypes.c_uint8 * max(n, 1)).from_buffer_copy(line or b"\0")
+    dst = (ctypes.c_uint8 * max(n, 1))()
+    k = lib.pm_parse_line(src, n, dst)
+    return bytes(dst[:k]) if k else None
+
+
+class Dictionary:
+    """Unique patterns of the -d files, first occurrence wins."""
+
+    def __init__(self, paths=None, patterns=None):
+        self.lib = load()
+        if paths is not None:
+            arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+            err = ctypes.create_string_buffer(512)
+            self.ptr = self.lib.pm_dict_load(arr, len(paths), err, 512)
+            if not self.ptr:
+                raise OSError(err.value.decode())
+        else:
+            self.ptr = self.lib.pm_dict_new()
+            for k, p in enumerate(patterns or []):
+                b = (ctypes.c_uint8 * max(len(p), 1)).from_buffer_copy(p or b"\0")
+                self.lib.pm_dict_add(self.ptr, b, len(p), 0, k + 1)
+            self.lib.pm_dict_finalize(self.ptr)
+        d = self.ptr.contents
+        self.n = d.n
+        self.max_len = d.max_len
+        self.lines_total = d.lines_total
+        self.lines_rejected = d.lines_rejected
+
+    def pattern(self, i):
+        p = self.ptr.contents.pats[i]
+        return p.file, p.line, ctypes.string_at(p.bytes, p.len)
+
+    def pattern_ptr(self, i):
+        """The pm_pattern_id_t of pattern i (address of its PmPattern)."""
+        return ctypes.addressof(self.ptr.contents.pats[i])
+
+    def patterns(self):
+        return [self.pattern(i)[2] for i in range(self.n)]
+
+    def codes(self):
+        """u32 (file << 24 | line) per pattern index."""
+        out = np.empty(self.n, dtype=np.uint32)
+        pats = self.ptr.contents.pats
+        for i in range(self.n):
+            out[i] = (pats[i].file << 24) | pats[i].line
+        return out
+
+    def parents(self):
+        """Index of the longest proper suffix that is a pattern, -1 if none."""
+        base = ctypes.addressof(self.ptr.contents.pats[0]) if self.n else 0
+        size = ctypes.sizeof(PmPattern)
+        out = np.full(self.n, -1, dtype=np.int64)
+        pats = self.ptr.contents.pats
+        for i in range(self.n):
+            par = pats[i].parent
+            if par:
+                out[i] = (ctypes.addressof(par.contents) - base) // size
+        return out
+
+    def __del__(self):
+        ptr = getattr(self, "ptr", None)
+        if ptr:
+            self.lib.pm_dict_free(ptr)
+            self.ptr = None
+
+
+def gen_stream(n, seed, mode=0, offset=0):
+    """Synthetic stream, host implementation."""
+    lib = load()
+    buf = np.empty(n, dtype=np.uint8)
+    lib.pm_gen_stream_host(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), offset, n, seed, mode)
+    return buf
+
+
+class HipMatcher:
+    """One GPU matcher instance ("rt" = reverse-trie kernel, "ac" = AC DFA)."""
+
+    def __init__(self, kind="rt"):
+        self.lib = load()
+        self.kind_name = kind
+        self.obj = self.lib.pm_hip_rt_create() if kind == "rt" else self.lib.pm_hip_ac_create()
+        self._codes = None
+        self._dict = None
+
+    # --- MpsElem -------------------------------------------------------
+    def add_pattern(self, pat: bytes, pattern_id=None):
+        self.lib.pm_hip_add_pattern(self.obj, pat, len(pat), pattern_id)
+
+    def add_dictionary(self, d: Dictionary):
+        fn = ctypes.cast(self.lib.pm_hip_add_pattern, ctypes.c_void_p)
+        self.lib.pm_dict_feed(d.ptr, self.obj, fn)
+        self._dict = d
+
+    def compile(self):
+        self.lib.pm_hip_compile(self.obj)
+        if self._dict is not None:
+            self._codes = self.gid_codes(self._dict.codes())
+
+    def read_char(self, c: int):
+        return self.lib.pm_hip_read_char(self.obj, bytes([c]))
+
+    def read_block_ids(self, data: bytes):
+        """pm_pattern_id_t per position (ints; 0 = null)."""
+        n = len(data)
+        out = (ctypes.c_void_p * max(n, 1))()
+        self.lib.pm_hip_read_block(self.obj, data, n, out)
+        return [x or 0 for x in out[:n]]
+
+    def total_mem(self):
+        return self.lib.pm_hip_total_mem(self.obj)
+
+    def reset(self):
+        self.lib.pm_hip_reset(self.obj)
+
+    def free(self):
+        if self.obj:
+            self.lib.pm_hip_free(self.obj)
+            self.obj = None
+
+    # --- batch ---------------------------------------------------------
+    def read_block_gids(self, data) -> np.ndarray:
+        arr = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray)
+                                   else data, dtype=np.uint8)
+        out = np.empty(len(arr), dtype=np.uint32)
+        self.lib.pm_hip_read_block_gid(self.obj, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(arr),
+                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+        return out
+
+    def gid_codes(self, index_codes: np.ndarray) -> np.ndarray:
+        """Table gid -> value, given a value per pattern index (add order)."""
+        P = self.lib.pm_hip_n_patterns(self.obj)
+        tab = np.zeros(P + 1, dtype=index_codes.dtype)
+        for g in range(1, P + 1):
+            tab[g] = index_codes[self.lib.pm_hip_gid_index(self.obj, g)]
+        return tab
+
+    def read_block_codes(self, data) -> np.ndarray:
+        """(file << 24 | line) per position, the golden-fixture format."""
+        return self._codes[self.read_block_gids(data)]
+
+    def scan_device(self, d_text_ptr, stream_start, pos0, n, d_out_ptr, d_count_ptr, stream_ptr):
+        rc = self.lib.pm_hip_scan_device(self.obj, d_text_ptr, stream_start, pos0, n, d_out_ptr, d_count_ptr,
+                                         stream_ptr)
+        if rc != 0:
+            raise RuntimeError(self.lib.pm_hip_last_error().decode())
+
+    @property
+    def kernel_kind(self):
+        return self.lib.pm_hip_kernel_kind(self.obj)
+
+    @property
+    def max_pattern_len(self):
+        return self.lib.pm_hip_max_pattern_len(self.obj)
+
+    @property
+    def table_bytes(self):
+        return self.lib.pm_hip_table_bytes(self.obj)
+
+    @property
+    def device_seconds(self):
+        return self.lib.pm_hip_device_seconds(self.obj)
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

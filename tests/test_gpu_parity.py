@@ -1,0 +1,279 @@
+"""GPU parity: both HIP kernels, through the C-ABI, against the oracle and
+the reference's golden vectors.  Bit-exact (integer ids per position)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import patternmatching_amd as pm
+from oracle_lib import DATA, GOLDEN, dict_paths, fnv1a64_codes, oracle_for
+
+pytestmark = pytest.mark.gpu
+
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+SHIP = np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8)
+KINDS = ["rt", "ac"]
+
+_m = {}
+
+
+def matcher(key, kind):
+    if (key, kind) not in _m:
+        d = pm.Dictionary(dict_paths(key))
+        m = pm.HipMatcher(kind)
+        m.add_dictionary(d)
+        m.compile()
+        assert m.kernel_kind == (pm.KIND_RT if kind == "rt" else pm.KIND_AC)
+        _m[(key, kind)] = m
+    m = _m[(key, kind)]
+    m.reset()
+    return m
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("key", ["et", "snort", "merged"])
+def test_ship_stream_golden(key, kind):
+    gold = np.fromfile(os.path.join(GOLDEN, f"ship_{key}.u32"), dtype="<u4")
+    got = matcher(key, kind).read_block_codes(SHIP)
+    bad = np.nonzero(got != gold)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("case", MANIFEST["digests"], ids=lambda d: f"{d['dict']}-s{d['seed']}-m{d['mode']}-n{d['n']}")
+def test_seeded_digests(case, kind):
+    m = matcher(case["dict"], kind)
+    codes = m.read_block_codes(pm.gen_stream(case["n"], case["seed"], case["mode"]))
+    assert int(np.count_nonzero(codes)) == case["nonnull"]
+    nz = np.nonzero(codes)[0][:len(case["first"])]
+    assert [[int(i), int(codes[i])] for i in nz] == case["first"]
+    assert fnv1a64_codes(codes) == case["fnv1a64"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_ship_x64_merged(kind):
+    import hashlib
+    codes = matcher("merged", kind).read_block_codes(np.tile(SHIP, 64))
+    g = MANIFEST["ship_x64_merged"]
+    assert int(np.count_nonzero(codes)) == g["nonnull"]
+    assert hashlib.sha256(codes.astype("<u4").tobytes()).hexdigest() == g["sha256"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_state_carries_across_read_block_calls(kind):
+    """read_block == n read_char calls, state carried across calls
+    (mps.h:41-42; measure.c:281-304 never resets between chunks)."""
+    m = matcher("merged", kind)
+    text = np.tile(SHIP, 4)
+    whole = m.read_block_codes(text)
+    m.reset()
+    rng = np.random.default_rng(3)
+    cuts = np.sort(rng.choice(np.arange(1, len(text)), size=40, replace=False))
+    cuts = np.concatenate([[0], [1, 2, 3, 17, 346, 347, 348], cuts, [len(text)]])
+    cuts = np.unique(cuts)
+    parts = [m.read_block_codes(text[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    assert np.array_equal(np.concatenate(parts), whole)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_read_char_per_byte(kind):
+    m = matcher("merged", kind)
+    o = oracle_for("merged")
+    o.reset()
+    exp = o.scan_codes(SHIP[:160])
+    d = m._dict
+    got = []
+    for c in SHIP[:160].tolist():
+        pid = m.read_char(c)
+        got.append(m.lib.pm_pattern_code(pid))
+    assert got == exp.tolist()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_read_block_returns_pattern_ids(kind):
+    """The ids handed to add_pattern come back verbatim (mps.h:35-37)."""
+    m = matcher("et", kind)
+    ids = m.read_block_ids(SHIP[:2000].tobytes())
+    d = m._dict
+    base = d.pattern_ptr(0)
+    import ctypes
+    size = ctypes.sizeof(pm._lib.PmPattern)
+    gold = np.fromfile(os.path.join(GOLDEN, "ship_et.u32"), dtype="<u4")[:2000]
+    codes = d.codes()
+    for j, pid in enumerate(ids):
+        if pid == 0:
+            assert gold[j] == 0
+        else:
+            assert (pid - base) % size == 0
+            assert codes[(pid - base) // size] == gold[j]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_empty_and_ragged_inputs(kind):
+    m = matcher("snort", kind)
+    assert m.read_block_codes(b"").size == 0
+    o = oracle_for("snort")
+    text = pm.gen_stream(5000, seed=21, mode=0)
+    o.reset()
+    exp = o.scan_codes(text)
+    for n in (1, 2, 3, 15, 16, 17, 31, 33, 1000, 4999):
+        m.reset()
+        assert np.array_equal(m.read_block_codes(text[:n]), exp[:n]), n
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_kmp_kat(kind):
+    """Core/src/kmprt.c:303-326: AAAAAAAAAAAAAAAAAB matches at 17 and 42."""
+    d = pm.Dictionary([os.path.join(DATA, "kmp_kat.dict")])
+    m = pm.HipMatcher(kind)
+    m.add_dictionary(d)
+    m.compile()
+    codes = m.read_block_codes(np.fromfile(os.path.join(DATA, "kmp_kat.stream"), dtype=np.uint8))
+    assert list(np.nonzero(codes)[0]) == [17, 42]
+    m.free()
+
+
+EDGE_DICTS = {
+    "one_byte": [b"a"],
+    "nul_high": [b"\x00", b"\xff\x00", b"\x00\x00\x00", b"\x80\x81\x82\x83"],
+    "nested": [b"abcdef", b"cdef", b"ef", b"f", b"zzzzzzzzzz", b"zz"],
+    "dense_short": [bytes([i]) for i in range(256)] + [bytes([i, j]) for i in range(0, 256, 7) for j in range(0, 256, 5)],
+    "long": [bytes(range(40, 240)), bytes(range(40, 240))[100:], b"x" * 300, b"x" * 299 + b"y"],
+}
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("name", list(EDGE_DICTS))
+def test_edge_dictionaries_brute_force(name, kind):
+    pats = EDGE_DICTS[name]
+    d = pm.Dictionary(patterns=pats)
+    m = pm.HipMatcher(kind)
+    m.add_dictionary(d)
+    m.compile()
+    rng = np.random.default_rng(9)
+    alphabet = np.unique(np.frombuffer(b"".join(pats), np.uint8))
+    text = rng.choice(alphabet, size=20000).astype(np.uint8)
+    if name == "long":
+        text[5000:5200] = np.frombuffer(bytes(range(40, 240)), np.uint8)
+        text[8000:8300] = ord("x")
+        text[9000:9299] = ord("x")
+        text[9299] = ord("y")
+    codes = {}
+    for i in range(d.n):
+        f, l, b = d.pattern(i)
+        codes[b] = (f << 24) | l
+    L = max(map(len, pats))
+    tb = text.tobytes()
+    exp = np.zeros(len(tb), np.uint32)
+    for i in range(len(tb)):
+        for k in range(min(L, i + 1), 0, -1):
+            c = codes.get(tb[i + 1 - k:i + 1])
+            if c is not None:
+                exp[i] = c
+                break
+    got = m.read_block_codes(text)
+    assert np.array_equal(got, exp)
+    m.free()
+
+
+def _torch():
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available()
+    return torch
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_device_generator_matches_host(kind):
+    torch = _torch()
+    n = (1 << 20) + 13
+    d = torch.empty(n, dtype=torch.uint8, device="cuda")
+    lib = pm.load()
+    assert lib.pm_hip_gen_stream_device(d.data_ptr(), 12345, n, 77, 0 if kind == "rt" else 1,
+                                        torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), pm.gen_stream(n, 77, 0 if kind == "rt" else 1, offset=12345))
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_scan_device_shards_with_context(kind):
+    """Shard exactness: a shard scanned with max_len-1 bytes of context equals
+    the same positions of one whole-stream scan."""
+    torch = _torch()
+    m = matcher("merged", kind)
+    text = np.tile(SHIP, 40)  # adversarial: deep states everywhere
+    whole = m.read_block_gids(text)
+    W = m.max_pattern_len - 1
+    dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    for a, b in ((0, 10240), (4096, 50000), (10240 * 7 + 16 * 5, 10240 * 39), (len(text) - 4000, len(text))):
+        a16 = a - a % 16
+        out = torch.zeros(b - a16, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        m.scan_device(dt.data_ptr(), max(0, a16 - W), a16, b - a16, out.data_ptr(), cnt.data_ptr(), s)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, whole[a16:b]), (a, b)
+        assert int(cnt.item()) == int(np.count_nonzero(whole[a16:b]))
+    # too little context is detectably wrong on this adversarial stream (W = 346 matters)
+    wrong = 0
+    for a in range(10240, 10240 * 30, 10240 + 32):
+        a -= a % 16
+        out = torch.zeros(512, dtype=torch.int32, device="cuda")
+        m.scan_device(dt.data_ptr(), a, a, 512, out.data_ptr(), None, s)
+        torch.cuda.synchronize()
+        wrong += int(np.count_nonzero(out.cpu().numpy().view(np.uint32) != whole[a:a + 512]))
+    assert wrong > 0
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_count_only_mode(kind):
+    torch = _torch()
+    m = matcher("snort", kind)
+    n = 3_000_017
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    pm.load().pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 5, 0, s)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    c1 = torch.zeros(1, dtype=torch.int64, device="cuda")
+    c2 = torch.zeros(1, dtype=torch.int64, device="cuda")
+    m.scan_device(dt.data_ptr(), 0, 0, n, out.data_ptr(), c1.data_ptr(), s)
+    m.scan_device(dt.data_ptr(), 0, 0, n, None, c2.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert int(c1.item()) == int(c2.item()) == int((out != 0).sum().item())
+    o = oracle_for("snort")
+    o.reset()
+    exp = o.scan_codes(dt[:n].cpu().numpy())
+    assert np.array_equal(m._codes[out.cpu().numpy().view(np.uint32)], exp)
+
+
+@pytest.mark.slow
+def test_full_size_snort_1gib_kernels_agree():
+    """BASELINE config 3 size (snort, 1 GiB): the two independent kernels agree
+    position by position, and sampled windows match the oracle."""
+    torch = _torch()
+    rt, ac = matcher("snort", "rt"), matcher("snort", "ac")
+    n = 1 << 30
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    pm.load().pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 1, 0, s)
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = torch.empty(n, dtype=torch.int32, device="cuda")
+    ca = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cb = torch.zeros(1, dtype=torch.int64, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), ca.data_ptr(), s)
+    ac.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), cb.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert int(ca.item()) == int(cb.item()) == int((a != 0).sum().item())
+    o = oracle_for("snort")
+    W = o.max_len - 1
+    rng = np.random.default_rng(0)
+    for off in rng.integers(W, n - 100000, size=6).tolist() + [n - 70000]:
+        o.reset()
+        seg = dt[off - W:off + 65536].cpu().numpy()
+        exp = o.scan_codes(seg)[W:]
+        got = rt._codes[a[off:off + 65536].cpu().numpy().view(np.uint32)]
+        assert np.array_equal(got, exp), off
+    del a, b, dt
+    torch.cuda.empty_cache()

@@ -1,0 +1,97 @@
+"""The flattened HBM images (csrc/pm_flatten.cpp) are exact: a numpy
+emulation of each kernel over them reproduces the oracle / the reference's
+golden vectors.  CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import patternmatching_amd as pm
+from oracle_lib import DATA, GOLDEN, dict_paths, oracle_for
+from table_emulator import FlatImage, dfa_scan, gid_to_code, rt_scan
+
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+SHIP = np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8)
+
+_imgs = {}
+
+
+def image(key, kind):
+    if (key, kind) not in _imgs:
+        d = pm.Dictionary(dict_paths(key))
+        img = FlatImage(d.patterns(), kind)
+        _imgs[(key, kind)] = (d, img, gid_to_code(img, d))
+    return _imgs[(key, kind)]
+
+
+@pytest.mark.parametrize("key", ["et", "snort", "merged"])
+def test_rt_image_ship_stream(key):
+    d, img, tab = image(key, pm.KIND_RT)
+    assert img.fits()
+    gold = np.fromfile(os.path.join(GOLDEN, f"ship_{key}.u32"), dtype="<u4")
+    got = tab[rt_scan(img, SHIP)]
+    assert np.array_equal(got, gold)
+
+
+@pytest.mark.parametrize("key,mode", [("et", 0), ("snort", 0), ("merged", 0), ("snort", 1)])
+def test_rt_image_random(key, mode):
+    d, img, tab = image(key, pm.KIND_RT)
+    text = pm.gen_stream(1 << 18, seed=11, mode=mode)
+    o = oracle_for(key)
+    o.reset()
+    assert np.array_equal(tab[rt_scan(img, text)], o.scan_codes(text))
+
+
+def test_rt_image_context():
+    """Positions scanned with only max_len-1 bytes of context are exact."""
+    d, img, tab = image("merged", pm.KIND_RT)
+    text = np.tile(SHIP, 3)
+    o = oracle_for("merged")
+    o.reset()
+    full = o.scan_codes(text)
+    W = d.max_len - 1
+    for start in (5000, 10240 + 77, 20000):
+        got = tab[rt_scan(img, text[start - W:], stream_start=0)][W:W + 3000]
+        assert np.array_equal(got, full[start:start + 3000])
+
+
+@pytest.mark.parametrize("key", ["et"])
+def test_dfa_image_ship_stream(key):
+    d, img, tab = image(key, pm.KIND_AC)
+    gold = np.fromfile(os.path.join(GOLDEN, f"ship_{key}.u32"), dtype="<u4")
+    assert np.array_equal(tab[dfa_scan(img, SHIP)], gold)
+
+
+def test_small_dictionaries():
+    """Edge dictionaries: one-byte patterns only, NUL/high bytes, nested suffixes."""
+    cases = [
+        [b"a"],
+        [b"\x00", b"\xff\x00", b"\x00\x00\x00"],
+        [b"abcdef", b"cdef", b"ef", b"f", b"zzzzzzzzzz", b"zz"],
+        [bytes([i]) for i in range(256)] + [bytes([i, j]) for i in range(0, 256, 7) for j in range(0, 256, 5)],
+        [b"AAAAAAAAAAAAAAAAAB"],
+    ]
+    rng = np.random.default_rng(5)
+    for pats in cases:
+        d = pm.Dictionary(patterns=pats)
+        img = FlatImage(d.patterns(), pm.KIND_RT)
+        dimg = FlatImage(d.patterns(), pm.KIND_AC)
+        tab = gid_to_code(img, d)
+        dtab = gid_to_code(dimg, d)
+        alphabet = np.unique(np.frombuffer(b"".join(pats), np.uint8))
+        text = rng.choice(alphabet, size=5000).astype(np.uint8)
+        # brute force: longest pattern that is a suffix of text[:i+1]
+        pset = {p: (0, k + 1) for k, p in enumerate(d.patterns())}
+        codes = {p: (f << 24) | l for p, (f, l) in zip(d.patterns(), [d.pattern(i)[:2] for i in range(d.n)])}
+        L = max(map(len, pats))
+        exp = np.zeros(len(text), np.uint32)
+        tb = text.tobytes()
+        for i in range(len(tb)):
+            for k in range(min(L, i + 1), 0, -1):
+                s = tb[i + 1 - k:i + 1]
+                if s in codes:
+                    exp[i] = codes[s]
+                    break
+        assert np.array_equal(tab[rt_scan(img, text)], exp), pats[:3]
+        assert np.array_equal(dtab[dfa_scan(dimg, text)], exp), pats[:3]
