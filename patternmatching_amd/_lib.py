@@ -110,6 +110,16 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: PyTorch-ROCm bundles its own
+    # libamdhip64.so (SONAME libamdhip64.so.7, NEEDED as "libamdhip64.so" by
+    # libtorch_hip).  Loading torch first makes libpm.so's libamdhip64.so.7
+    # resolve to that same runtime, so device pointers and streams are
+    # shared; loading libpm.so first would pull /opt/rocm's copy and torch
+    # would then load a second runtime and see no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: run `make -C patternmatching_amd/csrc` "
                            "(or __graft_entry__.build()); there is no CPU fallback")
