@@ -101,12 +101,19 @@ int pm_hip_device_count(void);
 /* hipSetDevice for C callers (the CLI's -g); 0 on success. */
 int pm_hip_set_device(int device);
 
+/* Timing-only ablation launches of the reverse-trie kernel (variant 0 =
+ * product kernel, 1 = no depth>=3 stage, 2 = streaming only, 3 = no LDS
+ * filter); blocks <= 0
+ * keeps the default grid.  Outputs of variants 1-2 are not match ids. */
+int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, uint32_t* d_out,
+                              unsigned long long* d_count, void* hip_stream, int blocks);
+
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */
 /* kind 1 = reverse-trie image, 2 = AC dense-DFA image */
 void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int kind);
 int pm_flat_fits(void* handle);
-/* name: "t12" "t3" "b2" "rec" "next" "out" "index_of_gid"; returns element count */
+/* name: "t12" "filt" "n2i" "t3" "rec" "next" "out" "index_of_gid"; returns element count */
 size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* elem_size);
 void pm_flat_free(void* handle);
 

@@ -94,6 +94,8 @@ SIGNATURES = {
     "pm_hip_last_error": (ctypes.c_char_p, []),
     "pm_hip_device_count": (ctypes.c_int, []),
     "pm_hip_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "pm_hip_debug_scan_variant": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int64, c_vp, c_vp, c_vp,
+                                                 ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
     "pm_flat_fits": (ctypes.c_int, [c_vp]),

@@ -125,7 +125,9 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
         if (t.depth[v] >= 3 && first_d3 == t.n) first_d3 = v;
     }
     im.nrec = t.n - first_d3;
-    im.fits = n_short < RT_CONT16 && im.n2int < RT_CONT16 && im.nrec < RT_CONT32;
+    uint32_t max_len = 0;
+    for (const auto& p : pats) max_len = std::max<uint32_t>(max_len, (uint32_t)p.size());
+    im.fits = n_short < RT_CONT16 && im.nrec < (1u << 22) && max_len <= 512;
     if (!im.fits) return im;
 
     im.t12.assign(RT_T1_BASE + 256, 0);
@@ -137,22 +139,45 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
             if (n1) {
                 uint32_t n2 = t.child(n1, c1);
                 if (!n2) v = best[n1];
-                else if (t.ccount[n2]) v = RT_CONT16 | n2i[n2];
-                else v = best[n2];
+                else v = (t.ccount[n2] ? RT_CONT16 : 0u) | best[n2];
             }
             im.t12[(c0 << 8) | c1] = (uint16_t)v;
         }
     }
-    im.t3.assign((size_t)im.n2int * 256, 0);
-    im.b2.assign(im.n2int, 0);
+    // depth-3 suffixes: filter bits + hash table
+    uint32_t d3 = 0;
+    for (uint32_t v = 1; v < t.n && t.depth[v] <= 2; ++v)
+        if (t.depth[v] == 2) d3 += t.ccount[v];
+    im.t3h_bits = 4;
+    while ((1u << im.t3h_bits) < 4 * d3) ++im.t3h_bits;
+    const uint32_t tmask = (1u << im.t3h_bits) - 1;
+    im.t3h.assign((size_t)4 << im.t3h_bits, 0);
+    im.filt.assign(RT_FILTER_WORDS, 0);
+    auto answer = [&](uint32_t v) { return t.ccount[v] ? (RT_CONT32 | (v - first_d3)) : best[v]; };
     for (uint32_t v = 1; v < t.n && t.depth[v] <= 2; ++v) {
-        if (n2i[v] == UINT32_MAX) continue;
-        uint32_t row = n2i[v];
-        im.b2[row] = best[v];
-        for (uint32_t c = 0; c < 256; ++c) im.t3[(size_t)row * 256 + c] = best[v];
+        if (t.depth[v] != 2 || !t.ccount[v]) continue;
+        const uint32_t c0 = t.label[t.parent[v]], c1 = t.label[v];
         for (uint32_t k = 0; k < t.ccount[v]; ++k) {
-            uint32_t n3 = t.cstart[v] + k;
-            im.t3[(size_t)row * 256 + t.label[n3]] = t.ccount[n3] ? (RT_CONT32 | (n3 - first_d3)) : best[n3];
+            const uint32_t n3 = t.cstart[v] + k;
+            const uint32_t c2 = t.label[n3];
+            const uint32_t key = c2 | (c1 << 8) | (c0 << 16);
+            const uint32_t h = pm_rt_hash(key);
+            const uint32_t w = (uint32_t)(((uint64_t)h * RT_FILTER_WORDS) >> 32);
+            im.filt[w] |= pm_rt_filter_mask(h);
+            uint32_t slot = h >> (32 - im.t3h_bits);
+            while (im.t3h[4 * (size_t)slot]) slot = (slot + 1) & tmask;
+            uint32_t* e = &im.t3h[4 * (size_t)slot];
+            const uint32_t kind = t.ccount[n3] == 0 ? 0u : (t.ccount[n3] == 1 ? 1u : 2u);
+            e[0] = (kind << 25) | RT_T3H_VALID | key;
+            e[1] = best[n3];
+            if (kind == 1) {
+                const uint32_t n4 = t.cstart[n3];
+                e[2] = t.label[n4];
+                e[3] = answer(n4);
+            } else if (kind == 2) {
+                e[3] = RT_CONT32 | (n3 - first_d3);
+            }
+            im.d3++;
         }
     }
     im.rec.assign((size_t)im.nrec * RT_REC_WORDS, 0);

@@ -7,9 +7,23 @@
 //           visits exactly the patterns that end at i; the deepest pattern
 //           node on the walk is the answer of read_char at i (the reference's
 //           "longest pattern ending here", mps.h:41-42 / mpac.c:318).
-//             t12   u16[65536 + 256]  depth<=2 in one lookup (LDS-resident)
-//             t3    u32[n2int * 256]  depth-3 step from internal depth-2 nodes
-//             b2    u32[n2int]        best pattern on the path to a depth-2 node
+//             t12   u16[65536 + 256]  depth<=2 in one lookup (first 64K
+//                                     LDS-resident): best pattern so far, bit
+//                                     15 set when the depth-2 node has children
+//             filt  u32[RT_FILTER_WORDS] blocked Bloom filter (2 bits per key)
+//                                     of the 3-byte suffixes that are depth-3
+//                                     nodes (LDS-resident): no false negatives
+//             t3h   u32x4[2^k]        open-addressing table of those suffixes
+//                                     (load factor <= 1/4), one 16-B entry per
+//                                     depth-3 node n3 that decides depth 4 too:
+//                                       x = kind << 25 | valid << 24 | key24
+//                                           (kind 0: n3 has no children,
+//                                            1: one child, 2: several)
+//                                       y = best pattern on the path to n3
+//                                       z = kind 1: the child's byte
+//                                       w = kind 1: the child's answer (gid,
+//                                           or RT_CONT32 | its record);
+//                                           kind 2: RT_CONT32 | n3's record
 //             rec   u32[nrec * 12]    48-B records for nodes of depth >= 3:
 //                                     child bitmap[8], child base, best, 8 u8
 //                                     prefix popcounts
@@ -32,15 +46,16 @@ struct PmGidMap {
 };
 
 struct RtImage {
-    bool fits = false;   // u16 t12 encoding possible (short patterns and n2int < 32768)
+    // encodings fit: fewer than 32768 patterns of length <= 2 (u16 t12),
+    // records < 2^22 and patterns <= 512 bytes (queued deep-walk items)
+    bool fits = false;
     std::vector<uint16_t> t12;
-    std::vector<uint32_t> t3;
-    std::vector<uint32_t> b2;
+    std::vector<uint32_t> filt;
+    std::vector<uint32_t> t3h;  // 4 words per entry
     std::vector<uint32_t> rec;
-    uint32_t n2int = 0, nrec = 0, nodes = 0;
-    size_t bytes() const {
-        return t12.size() * 2 + t3.size() * 4 + b2.size() * 4 + rec.size() * 4;
-    }
+    uint32_t t3h_bits = 0;
+    uint32_t n2int = 0, nrec = 0, nodes = 0, d3 = 0;
+    size_t bytes() const { return t12.size() * 2 + filt.size() * 4 + t3h.size() * 4 + rec.size() * 4; }
 };
 
 struct DfaImage {
@@ -57,6 +72,16 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g);
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g);
 
 constexpr uint32_t RT_T1_BASE = 65536;   // t12[65536 + c]: lookback of exactly one byte
-constexpr uint32_t RT_CONT16 = 0x8000u;  // t12: continue at internal depth-2 node (low 15 bits)
+constexpr uint32_t RT_CONT16 = 0x8000u;  // t12: depth-2 node has children (low 15 bits: best so far)
 constexpr uint32_t RT_CONT32 = 0x80000000u;  // t3: continue at record (low 31 bits)
 constexpr int RT_REC_WORDS = 12;
+constexpr uint32_t RT_FILTER_WORDS = 6144;  // 24 KiB of LDS
+
+// The filter's hash (host and device must agree): key24 = text[i-2] |
+// text[i-1] << 8 | text[i] << 16 (the little-endian u24 ending at i, so the
+// t12 index is key24 >> 8); h = key24 * 0x9E3779B1 (mod 2^32); filter word
+// = mulhi(h, RT_FILTER_WORDS), bits (h >> 4) & 31 and (h >> 9) & 31; t3h
+// slot = h >> (32 - t3h_bits), then linear probing.
+inline uint32_t pm_rt_hash(uint32_t k) { return k * 0x9E3779B1u; }
+inline uint32_t pm_rt_filter_mask(uint32_t h) { return (1u << ((h >> 4) & 31)) | (1u << ((h >> 9) & 31)); }
+constexpr uint32_t RT_T3H_VALID = 1u << 24;

@@ -4,10 +4,11 @@
 #include <cstdint>
 
 struct RtDev {
-    const uint16_t* t12;  // 65536 + 256 u16, staged into LDS per workgroup
-    const uint32_t* t3;   // n2int * 256
-    const uint32_t* b2;   // n2int
-    const uint32_t* rec;  // nrec * 12
+    const uint16_t* t12;   // 65536 + 256 u16; the first 64K staged into LDS per workgroup
+    const uint32_t* filt;  // RT_FILTER_WORDS u32, staged into LDS per workgroup
+    const uint4* t3h;      // 2^t3h_bits entries (pm_flatten.h)
+    const uint32_t* rec;   // nrec * 12
+    uint32_t t3h_bits;
 };
 
 struct DfaDev {
@@ -20,6 +21,10 @@ struct DfaDev {
 // pos0 % 16 == 0; out (n u32) may be null; count (u64) may be null.
 hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
                         unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s);
+// ablation variants of the RT kernel (timing only; see pm_kernels.hip)
+hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
+                                uint32_t* out, unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s,
+                                int blocks_override);
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s);
 hipError_t pm_launch_gen(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode, hipStream_t s);

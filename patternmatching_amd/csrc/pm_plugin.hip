@@ -203,8 +203,9 @@ void pm_hip_compile(void* obj) {
         RtImage im = pm_build_rt(o->pats, o->gids);
         if (im.fits) {
             o->rt.t12 = (const uint16_t*)dalloc_copy(o, im.t12.data(), im.t12.size() * 2);
-            o->rt.t3 = (const uint32_t*)dalloc_copy(o, im.t3.data(), im.t3.size() * 4);
-            o->rt.b2 = (const uint32_t*)dalloc_copy(o, im.b2.data(), im.b2.size() * 4);
+            o->rt.filt = (const uint32_t*)dalloc_copy(o, im.filt.data(), im.filt.size() * 4);
+            o->rt.t3h = (const uint4*)dalloc_copy(o, im.t3h.data(), im.t3h.size() * 4);
+            o->rt.t3h_bits = im.t3h_bits;
             o->rt.rec = (const uint32_t*)dalloc_copy(o, im.rec.data(), im.rec.size() * 4);
         } else {
             std::fprintf(stderr, "pm_hip: dictionary exceeds the reverse-trie u16 encoding; using the DFA kernel\n");
@@ -310,6 +311,16 @@ int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
     return 0;
 }
 
+// Timing-only ablation launches of the RT kernel (bench_variants.py).
+int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, uint32_t* d_out,
+                              unsigned long long* d_count, void* hip_stream, int blocks) {
+    PmHip* o = as(obj);
+    if (o->kind != KIND_RT) return -1;
+    hipError_t e = pm_launch_rt_variant(variant, d_text, 0, 0, n, d_out, d_count, o->rt, o->num_cu,
+                                        (hipStream_t)hip_stream, blocks);
+    return e == hipSuccess ? 0 : -3;
+}
+
 int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
                              void* hip_stream) {
     hipError_t e = pm_launch_gen(d_dst, offset, n, seed, mode, (hipStream_t)hip_stream);
@@ -372,8 +383,8 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
     };
     std::string s(name);
     if (s == "t12") return ret(h->rt.t12);
-    if (s == "t3") return ret(h->rt.t3);
-    if (s == "b2") return ret(h->rt.b2);
+    if (s == "filt") return ret(h->rt.filt);
+    if (s == "t3h") return ret(h->rt.t3h);
     if (s == "rec") return ret(h->rt.rec);
     if (s == "next") return ret(h->dfa.next);
     if (s == "out") return ret(h->dfa.out);

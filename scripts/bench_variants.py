@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Ablation timing of the RT kernel variants, interleaved rounds in one
+process (guide §5.4 rule 24).  Prints a JSON summary."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+import patternmatching_amd as pm  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--dict", default="snort")
+ap.add_argument("--bytes", type=int, default=1 << 30)
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--stream", type=int, default=0)
+ap.add_argument("--variants", default="0,1,2")
+ap.add_argument("--blocks", default="0")
+ap.add_argument("--modes", default="dense,count")
+args = ap.parse_args()
+DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
+data = os.path.join(REPO, "tests", "golden", "data")
+lib = pm.load()
+d = pm.Dictionary([os.path.join(data, x) for x in DICTS[args.dict]])
+m = pm.HipMatcher("rt")
+m.add_dictionary(d)
+m.compile()
+n = args.bytes
+s = torch.cuda.current_stream()
+text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, 1, args.stream, s.cuda_stream)
+out = torch.empty(n, dtype=torch.int32, device="cuda")
+cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+variants = [(int(v), mode, int(b)) for v in args.variants.split(",") for mode in args.modes.split(",")
+            for b in args.blocks.split(",")]
+times = {k: [] for k in variants}
+for r in range(args.rounds + 1):
+    for (v, mode, b) in variants:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        rc = lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, out.data_ptr() if mode == "dense" else None,
+                                           cnt.data_ptr(), s.cuda_stream, b)
+        assert rc == 0
+        e1.record(s)
+        torch.cuda.synchronize()
+        if r:
+            times[(v, mode, b)].append(e0.elapsed_time(e1))
+res = {}
+if "9" in args.variants.split(","):
+    for mode in ("dense", "count"):
+        cnt.zero_()
+        lib.pm_hip_debug_scan_variant(m.obj, 9, text.data_ptr(), n, out.data_ptr() if mode == "dense" else None,
+                                      cnt.data_ptr(), s.cuda_stream, 0)
+        torch.cuda.synchronize()
+        c = [int(x) for x in cnt.tolist()]
+        names = ["lds_filter", "push", "resolve", "pull", "store", "rounds", "chunks", "total"]
+        res[f"v9-stamps-{mode}"] = {k: (c[i] / c[6] if i < 5 or i == 7 else c[i]) for i, k in enumerate(names)}
+for v in (7, 8):
+    if str(v) in args.variants.split(","):
+        cnt.zero_()
+        lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, None, cnt.data_ptr(), s.cuda_stream, 0)
+        torch.cuda.synchronize()
+        res[f"v{v}-counter"] = {"value": int(cnt.item()), "per_position": int(cnt.item()) / n}
+for (v, mode, b), t in times.items():
+    if v in (7, 8, 9):
+        continue
+    ms = statistics.median(t)
+    res[f"v{v}-{mode}-b{b}"] = {"ms": round(ms, 4), "min": round(min(t), 4), "GBps_stream": round(n / ms / 1e6, 1),
+                                "alg_GBps": round(n * (5 if mode == "dense" else 1) / ms / 1e6, 1)}
+print(json.dumps(res, indent=1))

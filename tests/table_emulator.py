@@ -25,7 +25,7 @@ class FlatImage:
         data = ctypes.c_void_p()
         es = ctypes.c_size_t()
         n = self.lib.pm_flat_array(self.h, name.encode(), ctypes.byref(data), ctypes.byref(es))
-        dt = {2: np.uint16, 4: np.uint32}[es.value] if es.value else np.uint32
+        dt = {2: np.uint16, 4: np.uint32, 8: np.uint64}[es.value] if es.value else np.uint32
         if n == 0:
             return np.zeros(0, dt)
         buf = (ctypes.c_char * (n * es.value)).from_address(data.value)
@@ -36,11 +36,54 @@ class FlatImage:
             self.lib.pm_flat_free(self.h)
 
 
-def rt_scan(img, text, stream_start=0):
+FILTER_WORDS = 6144
+
+
+def rt_hash(k):
+    """pm_rt_hash: key24 * 0x9E3779B1 mod 2^32."""
+    return (np.asarray(k).astype(np.uint64) * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)
+
+
+def filter_maybe(filt, key24):
+    h = rt_hash(key24)
+    w = filt[((h * np.uint64(FILTER_WORDS)) >> np.uint64(32)).astype(np.int64)].astype(np.uint64)
+    m = (np.uint64(1) << ((h >> np.uint64(4)) & np.uint64(31))) | (np.uint64(1) << ((h >> np.uint64(9)) & np.uint64(31)))
+    return (w & m) == m
+
+
+def t3h_lookup(t3h, bits, key24):
+    """The 4-word entry of key24, or None."""
+    mask = (1 << bits) - 1
+    slot = int(rt_hash(np.array([key24], np.uint32))[0]) >> (32 - bits)
+    while True:
+        e = t3h[4 * slot:4 * slot + 4]
+        if not int(e[0]) & (1 << 24):
+            return None
+        if int(e[0]) & 0xFFFFFF == key24:
+            return [int(x) for x in e]
+        slot = (slot + 1) & mask
+
+
+def rec_walk(rec, text, p, avail, node, d):
+    while True:
+        R = rec[node]
+        if d >= avail:
+            return int(R[9])
+        c = int(text[p - d])
+        w, bit = c >> 5, c & 31
+        if not (int(R[w]) >> bit) & 1:
+            return int(R[9])
+        pre = (int(R[10 + (w >> 2)]) >> (8 * (w & 3))) & 0xFF
+        node = int(R[8]) + pre + bin(int(R[w]) & ((1 << bit) - 1)).count("1")
+        d += 1
+
+
+def rt_scan(img, text, stream_start=0, use_filter=True):
     """gids for every position of text (stream begins at stream_start)."""
     t12 = img.array("t12").astype(np.uint32)
-    t3 = img.array("t3")
-    b2 = img.array("b2")
+    filt = img.array("filt")
+    t3h = img.array("t3h")
+    bits = int(len(t3h) // 4).bit_length() - 1
     rec = img.array("rec").reshape(-1, 12)
     text = np.asarray(text, dtype=np.uint8)
     n = len(text)
@@ -50,31 +93,28 @@ def rt_scan(img, text, stream_start=0):
     c1 = np.concatenate([[0], text[:-1]]).astype(np.uint32)
     c2 = np.concatenate([[0, 0], text[:-2]]).astype(np.uint32)
     v = t12[(c0 << 8) | c1]
-    out = v.copy()
+    out = v & 0x7FFF
     out[avail == 1] = t12[65536 + c0[avail == 1]]
-    cont = (v & 0x8000) != 0
-    m2 = cont & (avail == 2)
-    out[m2] = b2[v[m2] & 0x7FFF]
-    m3 = cont & (avail >= 3)
-    r = t3[(v[m3] & 0x7FFF).astype(np.int64) * 256 + c2[m3]]
-    out[m3] = r
-    deep_pos = i[m3][(r & 0x80000000) != 0]
-    for p in deep_pos:
-        node = int(out[p]) & 0x7FFFFFFF
-        d = 3
-        while True:
-            R = rec[node]
-            if d >= avail[p]:
-                out[p] = R[9]
-                break
-            c = int(text[p - d])
-            w, bit = c >> 5, c & 31
-            if not (int(R[w]) >> bit) & 1:
-                out[p] = R[9]
-                break
-            pre = (int(R[10 + (w >> 2)]) >> (8 * (w & 3))) & 0xFF
-            node = int(R[8]) + pre + bin(int(R[w]) & ((1 << bit) - 1)).count("1")
-            d += 1
+    key24 = c2 | (c1 << 8) | (c0 << 16)
+    cont = ((v & 0x8000) != 0) & (avail >= 3)
+    if use_filter:
+        cont &= filter_maybe(filt, key24)
+    for p in i[cont]:
+        e = t3h_lookup(t3h, bits, int(key24[p]))
+        if e is None:
+            continue  # best2 stays
+        kind = e[0] >> 25
+        if kind == 0 or avail[p] < 4:
+            out[p] = e[1]
+        elif kind == 1:
+            if int(text[p - 3]) != e[2]:
+                out[p] = e[1]
+            elif not e[3] & 0x80000000:
+                out[p] = e[3]
+            else:
+                out[p] = rec_walk(rec, text, p, avail[p], e[3] & 0x7FFFFFFF, 4)
+        else:
+            out[p] = rec_walk(rec, text, p, avail[p], e[3] & 0x7FFFFFFF, 3)
     return out
 
 

@@ -277,3 +277,29 @@ def test_full_size_snort_1gib_kernels_agree():
         assert np.array_equal(got, exp), off
     del a, b, dt
     torch.cuda.empty_cache()
+
+
+def test_adversarial_stream_large_rt_equals_ac():
+    """A 32 MiB tiling of the shipped adversarial stream queues far more
+    positions than the worklist holds, so the scan kernel's in-kernel
+    fallback runs; RT must still equal the independent AC-DFA kernel and the
+    oracle."""
+    torch = _torch()
+    rt, ac = matcher("merged", "rt"), matcher("merged", "ac")
+    n = 32 << 20
+    text = np.tile(SHIP, n // len(SHIP) + 1)[:n]
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = torch.empty(n, dtype=torch.int32, device="cuda")
+    ca = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cb = torch.zeros(1, dtype=torch.int64, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), ca.data_ptr(), s)
+    ac.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), cb.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert int(ca.item()) == int(cb.item()) == int((a != 0).sum().item())
+    o = oracle_for("merged")
+    o.reset()
+    exp = o.scan_codes(text[:1 << 20])
+    assert np.array_equal(rt._codes[a[:1 << 20].cpu().numpy().view(np.uint32)], exp)

@@ -40,7 +40,34 @@ def test_rt_image_random(key, mode):
     text = pm.gen_stream(1 << 18, seed=11, mode=mode)
     o = oracle_for(key)
     o.reset()
-    assert np.array_equal(tab[rt_scan(img, text)], o.scan_codes(text))
+    exp = o.scan_codes(text)
+    assert np.array_equal(tab[rt_scan(img, text)], exp)
+    assert np.array_equal(tab[rt_scan(img, text, use_filter=False)], exp)
+
+
+@pytest.mark.parametrize("key", ["et", "snort", "merged"])
+def test_rt_filter_has_no_false_negatives_and_few_positives(key):
+    """Every depth-3 suffix is in the LDS filter; on random ASCII the filter
+    passes only a few percent of depth-2 continuations."""
+    from table_emulator import filter_maybe
+    d, img, tab = image(key, pm.KIND_RT)
+    filt = img.array("filt")
+    t3h = img.array("t3h")[0::4]
+    valid = (t3h & (1 << 24)) != 0
+    keys = (t3h[valid] & 0xFFFFFF).astype(np.uint32)
+    assert len(keys) == len(set(keys.tolist())) > 1000
+    t12 = img.array("t12")
+    # every key sits under a depth-2 node with children
+    assert np.all(t12[keys >> 8] & 0x8000)
+    assert filter_maybe(filt, keys).all()
+    text = pm.gen_stream(1 << 18, seed=12, mode=0)
+    c0 = text.astype(np.uint32)[2:]
+    c1 = text.astype(np.uint32)[1:-1]
+    c2 = text.astype(np.uint32)[:-2]
+    cont = (t12[(c0 << 8) | c1] & 0x8000) != 0
+    passed = filter_maybe(filt, c2 | (c1 << 8) | (c0 << 16)) & cont
+    assert cont.mean() > 0.2
+    assert passed.mean() < 0.03, passed.mean()
 
 
 def test_rt_image_context():
