@@ -161,7 +161,8 @@ def main():
         alg_per_pos = 5 if args.mode == "dense" else 1  # 1 B read + 4 B id written (dense)
         achieved = n * alg_per_pos / (kernel_ms * 1e-3) / 1e9
         workload_key = f"{args.dict}-{args.stream}-{n}-{args.mode}-{args.kernel}"
-        traffic = load_traffic(workload_key)
+        tr = load_traffic(workload_key)
+        traffic = tr["traffic_bytes"] if tr else None
         res = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -195,6 +196,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": tr["source"] if tr else None,
                 "algorithmic_bytes_per_launch": n * alg_per_pos,
             },
             "cpu_baseline": cpu,
