@@ -2,6 +2,7 @@
 #include "pm_flatten.h"
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <unordered_map>
 
@@ -144,16 +145,15 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
             im.t12[(c0 << 8) | c1] = (uint16_t)v;
         }
     }
-    // depth-3 suffixes: filter bits + hash table
+    // depth-3 suffixes: filter bits + a two-choice cuckoo table (each key in
+    // slot h1 or h2, so a lookup is two independent loads and no chain)
     uint32_t d3 = 0;
     for (uint32_t v = 1; v < t.n && t.depth[v] <= 2; ++v)
         if (t.depth[v] == 2) d3 += t.ccount[v];
-    im.t3h_bits = 4;
-    while ((1u << im.t3h_bits) < 4 * d3) ++im.t3h_bits;
-    const uint32_t tmask = (1u << im.t3h_bits) - 1;
-    im.t3h.assign((size_t)4 << im.t3h_bits, 0);
     im.filt.assign(RT_FILTER_WORDS, 0);
     auto answer = [&](uint32_t v) { return t.ccount[v] ? (RT_CONT32 | (v - first_d3)) : best[v]; };
+    std::vector<std::array<uint32_t, 4>> ents;
+    ents.reserve(d3);
     for (uint32_t v = 1; v < t.n && t.depth[v] <= 2; ++v) {
         if (t.depth[v] != 2 || !t.ccount[v]) continue;
         const uint32_t c0 = t.label[t.parent[v]], c1 = t.label[v];
@@ -161,24 +161,52 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
             const uint32_t n3 = t.cstart[v] + k;
             const uint32_t c2 = t.label[n3];
             const uint32_t key = c2 | (c1 << 8) | (c0 << 16);
-            const uint32_t h = pm_rt_hash(key);
-            const uint32_t w = (uint32_t)(((uint64_t)h * RT_FILTER_WORDS) >> 32);
-            im.filt[w] |= pm_rt_filter_mask(h);
-            uint32_t slot = h >> (32 - im.t3h_bits);
-            while (im.t3h[4 * (size_t)slot]) slot = (slot + 1) & tmask;
-            uint32_t* e = &im.t3h[4 * (size_t)slot];
-            const uint32_t kind = t.ccount[n3] == 0 ? 0u : (t.ccount[n3] == 1 ? 1u : 2u);
+            const uint32_t f = pm_rt_fhash(key);
+            im.filt[pm_rt_filter_word(f)] |= pm_rt_filter_mask(f);
+            std::array<uint32_t, 4> e{};
+            const uint32_t nch = t.ccount[n3];
+            const uint32_t kind = nch == 0 ? 0u : (nch <= RT_T3H_INLINE ? 1u : 2u);
             e[0] = (kind << 25) | RT_T3H_VALID | key;
             e[1] = best[n3];
             if (kind == 1) {
-                const uint32_t n4 = t.cstart[n3];
-                e[2] = t.label[n4];
-                e[3] = answer(n4);
+                // up to three child bytes inline; the child's answer inline
+                // for one child, else the first child's record (contiguous)
+                e[2] = nch << 24;
+                for (uint32_t j = 0; j < nch; ++j) e[2] |= (uint32_t)t.label[t.cstart[n3] + j] << (8 * j);
+                e[3] = nch == 1 ? answer(t.cstart[n3]) : t.cstart[n3] - first_d3;
             } else if (kind == 2) {
                 e[3] = RT_CONT32 | (n3 - first_d3);
             }
-            im.d3++;
+            ents.push_back(e);
         }
+    }
+    im.d3 = (uint32_t)ents.size();
+    for (im.t3h_bits = 4; (1u << im.t3h_bits) < 2 * im.d3; ++im.t3h_bits) {}
+    for (;; ++im.t3h_bits) {  // load <= 1/2: two-choice cuckoo insertion virtually never fails; grow if it does
+        const uint32_t bits = im.t3h_bits;
+        im.t3h.assign((size_t)4 << bits, 0);
+        bool ok = true;
+        auto empty = [&](uint32_t sl) { return !(im.t3h[4 * (size_t)sl] & RT_T3H_VALID); };
+        for (size_t q = 0; q < ents.size() && ok; ++q) {
+            std::array<uint32_t, 4> cur = ents[q];
+            const uint32_t k = cur[0] & 0xFFFFFFu;
+            uint32_t slot = pm_rt_slot1(k, bits);
+            if (!empty(slot) && empty(pm_rt_slot2(k, bits))) slot = pm_rt_slot2(k, bits);
+            // cuckoo walk: take the slot, re-home its occupant in its other slot
+            for (int kick = 0;; ++kick) {
+                uint32_t* e = &im.t3h[4 * (size_t)slot];
+                std::array<uint32_t, 4> ev;
+                std::memcpy(ev.data(), e, 16);
+                std::memcpy(e, cur.data(), 16);
+                if (!(ev[0] & RT_T3H_VALID)) break;
+                if (kick > 1000) { ok = false; break; }
+                cur = ev;
+                const uint32_t ke = cur[0] & 0xFFFFFFu;
+                const uint32_t e1 = pm_rt_slot1(ke, bits), e2 = pm_rt_slot2(ke, bits);
+                slot = slot == e1 ? e2 : e1;
+            }
+        }
+        if (ok) break;
     }
     im.rec.assign((size_t)im.nrec * RT_REC_WORDS, 0);
     for (uint32_t v = first_d3; v < t.n; ++v) {

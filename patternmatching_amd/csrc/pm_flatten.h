@@ -10,19 +10,24 @@
 //             t12   u16[65536 + 256]  depth<=2 in one lookup (first 64K
 //                                     LDS-resident): best pattern so far, bit
 //                                     15 set when the depth-2 node has children
-//             filt  u32[RT_FILTER_WORDS] blocked Bloom filter (2 bits per key)
+//             filt  u32[RT_FILTER_WORDS] blocked Bloom filter (3 bits per key)
 //                                     of the 3-byte suffixes that are depth-3
 //                                     nodes (LDS-resident): no false negatives
 //             t3h   u32x4[2^k]        open-addressing table of those suffixes
-//                                     (load factor <= 1/4), one 16-B entry per
+//                                     (two-choice cuckoo, load <= 1/2), one 16-B entry per
 //                                     depth-3 node n3 that decides depth 4 too:
 //                                       x = kind << 25 | valid << 24 | key24
 //                                           (kind 0: n3 has no children,
-//                                            1: one child, 2: several)
+//                                            1: one to three children,
+//                                            2: more)
 //                                       y = best pattern on the path to n3
-//                                       z = kind 1: the child's byte
-//                                       w = kind 1: the child's answer (gid,
-//                                           or RT_CONT32 | its record);
+//                                       z = kind 1: child bytes (byte k =
+//                                           child k, sorted) | count << 24
+//                                       w = kind 1, one child: the child's
+//                                           answer (gid, or RT_CONT32 | its
+//                                           record); several: the record of
+//                                           the first child (children are
+//                                           contiguous);
 //                                           kind 2: RT_CONT32 | n3's record
 //             rec   u32[nrec * 12]    48-B records for nodes of depth >= 3:
 //                                     child bitmap[8], child base, best, 8 u8
@@ -75,13 +80,21 @@ constexpr uint32_t RT_T1_BASE = 65536;   // t12[65536 + c]: lookback of exactly 
 constexpr uint32_t RT_CONT16 = 0x8000u;  // t12: depth-2 node has children (low 15 bits: best so far)
 constexpr uint32_t RT_CONT32 = 0x80000000u;  // t3: continue at record (low 31 bits)
 constexpr int RT_REC_WORDS = 12;
-constexpr uint32_t RT_FILTER_WORDS = 6144;  // 24 KiB of LDS
+constexpr uint32_t RT_FILTER_WORDS = 4096;  // 16 KiB of LDS
 
-// The filter's hash (host and device must agree): key24 = text[i-2] |
-// text[i-1] << 8 | text[i] << 16 (the little-endian u24 ending at i, so the
-// t12 index is key24 >> 8); h = key24 * 0x9E3779B1 (mod 2^32); filter word
-// = mulhi(h, RT_FILTER_WORDS), bits (h >> 4) & 31 and (h >> 9) & 31; t3h
-// slot = h >> (32 - t3h_bits), then linear probing.
+// Hashes (host and device must agree).  key24 = text[i-2] | text[i-1] << 8
+// | text[i] << 16 (the little-endian u24 ending at i, so the t12 index is
+// key24 >> 8).  Filter: f = key24 * 0x9E3779 (mod 2^32; one full-rate 24-bit
+// multiply on the device), word f >> 20, bits (f >> 5), (f >> 10) and
+// (f >> 15) (& 31).  t3h: a key sits in slot pm_rt_slot1 (h >> (32 -
+// t3h_bits), h = key24 * 0x9E3779B1) or pm_rt_slot2.
 inline uint32_t pm_rt_hash(uint32_t k) { return k * 0x9E3779B1u; }
-inline uint32_t pm_rt_filter_mask(uint32_t h) { return (1u << ((h >> 4) & 31)) | (1u << ((h >> 9) & 31)); }
+inline uint32_t pm_rt_fhash(uint32_t k) { return k * 0x9E3779u; }
+inline uint32_t pm_rt_filter_word(uint32_t f) { return f >> 20; }
+inline uint32_t pm_rt_filter_mask(uint32_t f) {
+    return (1u << ((f >> 5) & 31)) | (1u << ((f >> 10) & 31)) | (1u << ((f >> 15) & 31));
+}
 constexpr uint32_t RT_T3H_VALID = 1u << 24;
+inline uint32_t pm_rt_slot1(uint32_t k, uint32_t bits) { return pm_rt_hash(k) >> (32 - bits); }
+inline uint32_t pm_rt_slot2(uint32_t k, uint32_t bits) { return (k * 0x85EBCA77u) >> (32 - bits); }
+constexpr uint32_t RT_T3H_INLINE = 3;  // child bytes held in a t3h entry

@@ -3,11 +3,14 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+constexpr size_t RT_SCRATCH_BYTES = 4096;
+
 struct RtDev {
     const uint16_t* t12;   // 65536 + 256 u16; the first 64K staged into LDS per workgroup
     const uint32_t* filt;  // RT_FILTER_WORDS u32, staged into LDS per workgroup
     const uint4* t3h;      // 2^t3h_bits entries (pm_flatten.h)
     const uint32_t* rec;   // nrec * 12
+    uint32_t* scratch;     // RT_SCRATCH_BYTES the kernel may overwrite (stand-in stores)
     uint32_t t3h_bits;
 };
 

@@ -34,16 +34,27 @@ namespace {
 constexpr int RT_THREADS = 1024;
 constexpr int RT_WAVES = RT_THREADS / 64;
 constexpr int RT_T2_U16 = 65536;
-constexpr int RT_FILTER_WORDS = 6144;  // must match pm_flatten.h
-constexpr int RT_QCAP = 64;            // queue items per wave (one per lane per round)
-constexpr uint32_t RT_QFLUSH = 40;     // resolve once this many are queued
+constexpr int RT_FILTER_WORDS = 4096;  // must match pm_flatten.h
+constexpr uint32_t RT_QCAP = 128;       // queue ring per wave (power of two)
+constexpr uint32_t RT_ROUND = 64;       // items per round (one per lane)
 constexpr int RT_CHUNK = 1024;         // positions per wave iteration
 constexpr uint32_t CONT16 = 0x8000u;
 constexpr uint32_t CONT32 = 0x80000000u;
 constexpr uint32_t T3H_VALID = 1u << 24;
 
 __device__ __forceinline__ uint32_t rt_hash(uint32_t k) { return k * 0x9E3779B1u; }  // pm_rt_hash
-__device__ __forceinline__ uint32_t rt_fmask(uint32_t h) { return (1u << ((h >> 4) & 31)) | (1u << ((h >> 9) & 31)); }
+// pm_rt_fhash: k < 2^24, so this is one full-rate v_mul_u32_u24 (written
+// out: the compiler loses the 24-bit range through the byte extraction and
+// would emit the quarter-rate v_mul_lo_u32)
+__device__ __forceinline__ uint32_t rt_fhash(uint32_t k) {
+    uint32_t h;
+    asm("v_mul_u32_u24 %0, 0x9e3779, %1" : "=v"(h) : "v"(k));
+    return h;
+}
+// the three filter bits of f present in word w (shift amounts use bits 0-4)
+__device__ __forceinline__ uint32_t rt_fhit(uint32_t w, uint32_t f) {
+    return (w >> ((f >> 5) & 31)) & (w >> ((f >> 10) & 31)) & (w >> ((f >> 15) & 31)) & 1u;
+}
 
 __device__ __forceinline__ uint64_t stamp() {
     uint64_t t;
@@ -51,6 +62,18 @@ __device__ __forceinline__ uint64_t stamp() {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     __builtin_amdgcn_sched_barrier(0);
     return t;
+}
+
+// Inclusive prefix sum over the 64 lanes: row_shr 1/2/4/8 within rows of 16,
+// then row_bcast 15 / 31 across rows (lanes without a source add 0).
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
 }
 
 __device__ __forceinline__ uint32_t wave_prefix(uint64_t m) {
@@ -76,25 +99,29 @@ __device__ __forceinline__ uint32_t rt_deep(const uint8_t* __restrict__ text, co
     }
 }
 
+__device__ __forceinline__ uint32_t rt_slot1(uint32_t k, uint32_t bits) { return rt_hash(k) >> (32 - bits); }
+__device__ __forceinline__ uint32_t rt_slot2(uint32_t k, uint32_t bits) { return (k * 0x85EBCA77u) >> (32 - bits); }
+
 // The walk past depth 2 from key24 = text[i-2] | text[i-1] << 8 | text[i] << 16
 // (a depth-2 node with children) with c3 = text[i-3] when avail >= 4;
-// best2 = the answer if it stops at depth 2.  One probe of t3h decides
-// depth 3 and, for nodes with at most one child, depth 4.
+// best2 = the answer if it stops at depth 2.  The t3h entry of key24 (slot1
+// or slot2) decides depth 3 and, for nodes with at most three children,
+// whether the walk goes on past depth 4.
 __device__ __forceinline__ uint32_t rt_from_d2(const uint8_t* __restrict__ text, const RtDev& t, uint32_t key24,
                                                uint32_t c3, uint32_t best2, int64_t i, int64_t avail) {
-    const uint32_t mask = (1u << t.t3h_bits) - 1u;
-    uint32_t slot = rt_hash(key24) >> (32 - t.t3h_bits);
-    uint4 e;
-    for (;;) {
-        e = t.t3h[slot];
-        if (!(e.x & T3H_VALID)) return best2;
-        if ((e.x & 0xFFFFFFu) == key24) break;
-        slot = (slot + 1) & mask;
+    const uint32_t want = T3H_VALID | key24;
+    uint4 e = t.t3h[rt_slot1(key24, t.t3h_bits)];
+    if ((e.x & 0x1FFFFFFu) != want) {
+        e = t.t3h[rt_slot2(key24, t.t3h_bits)];
+        if ((e.x & 0x1FFFFFFu) != want) return best2;
     }
     const uint32_t kind = e.x >> 25;
     if (kind == 0 || avail < 4) return e.y;
     if (kind == 1) {
-        if (c3 != e.z) return e.y;
+        const uint32_t nch = e.z >> 24;
+        const uint32_t k = c3 == (e.z & 0xFFu) ? 0u : c3 == ((e.z >> 8) & 0xFFu) ? 1u : c3 == ((e.z >> 16) & 0xFFu) ? 2u : 3u;
+        if (k >= nch) return e.y;
+        if (nch > 1) return rt_deep(text, t.rec, e.w + k, i, avail, 4);
         if (!(e.w & CONT32)) return e.w;
         return rt_deep(text, t.rec, e.w & 0x7FFFFFFFu, i, avail, 4);
     }
@@ -118,16 +145,17 @@ __device__ uint32_t rt_one(const uint8_t* __restrict__ text, const uint16_t* s_t
 //   1 = loads + t12 lookups + stores (no filter, no queue)
 //   2 = loads + stores only (streaming floor of this access pattern)
 //   9 = product kernel with s_memtime stamps per phase (diagnostic: count
-//       receives 8 u64 cycle sums: lds+filter, push, resolve, pull, store,
-//       rounds, chunks, total)
-template <int V>
+//       receives 8 u64 cycle sums: lds+filter, push, round wait, consume,
+//       store, issue, chunks, total)
+// DENSE: write the per-position ids (read_block); else count only.
+template <int V, bool DENSE>
 __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
                                                              int64_t pos0, int64_t n, uint32_t* __restrict__ out,
                                                              unsigned long long* __restrict__ count, RtDev t) {
     __shared__ __attribute__((aligned(16))) uint16_t s_t[RT_T2_U16];
     __shared__ __attribute__((aligned(16))) uint32_t s_f[RT_FILTER_WORDS];
-    __shared__ uint32_t s_qkey[RT_WAVES][RT_QCAP];  // key24 | text[i-3] << 24
-    __shared__ uint32_t s_qpos[RT_WAVES][RT_QCAP];  // position - pos0
+    __shared__ uint32_t s_qkey[RT_WAVES][RT_QCAP];  // 16 + 16 + 128 KiB: all of the CU's LDS
+    __shared__ uint32_t s_qpos[RT_WAVES][RT_QCAP];
     {
         const uint4* src = reinterpret_cast<const uint4*>(t.t12);
         uint4* dst = reinterpret_cast<uint4*>(s_t);
@@ -148,142 +176,283 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tA = 0, tB = 0;
     if (V == 9) tA = stamp();
+    // chunk c is "fast" (main loop) when all of it is in range and it starts
+    // >= 2 bytes into the stream: chunks [c_lo, c_hi)
     const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
+    const int64_t c_hi = n / RT_CHUNK;
+    const int64_t c_lo = pos0 - stream_start >= 2 ? 0 : 1;
     const int64_t stride = (int64_t)gridDim.x * RT_WAVES;
-    // a chunk is "fast" when all of it (and the 4 bytes before it) is in range
-    // and it starts >= 2 bytes into the stream
-    auto is_fast = [&](int64_t c) {
-        const int64_t pc = pos0 + c * RT_CHUNK;
-        return c < nchunks && pc + RT_CHUNK <= pos0 + n && pc - stream_start >= 2;
-    };
+    // out-of-range prefetches read this instead (any >= 1 KiB of table)
+    const uint8_t* dummy = reinterpret_cast<const uint8_t*>(t.filt) + 4;
     using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
     using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
-    // Queued positions carry over chunks; a round resolves the queue once it
-    // holds RT_QFLUSH items (or is full), so one round's latency is shared by
-    // several chunks.  Each chunk is stored before its positions can be
-    // resolved: a round's probes are issued after those stores and waited
-    // for, and vmcnt counts loads and stores in one in-order queue, so every
-    // store is complete at L2 before a patch overwrites one of its
-    // placeholders (a line this CU wrote a few chunks ago, still in L2).
-    uint32_t qn = 0;  // items queued (wave-uniform)
-    auto flush = [&]() {
-        __builtin_amdgcn_wave_barrier();
-        if (V == 9) { const uint64_t u = stamp(); ph[1] += u - tB; tB = u; ph[5] += 1; }
-        if ((uint32_t)lane < qn) {
-            const uint32_t qk = qkey[lane];
-            const uint32_t k = qk & 0xFFFFFFu;
-            const int64_t i = pos0 + (int64_t)qpos[lane];
-            const uint32_t best2 = s_t[k >> 8] & 0x7FFFu;
-            const uint32_t v = rt_from_d2(text, t, k, qk >> 24, best2, i, i - stream_start + 1);
-            cnt += (uint32_t)(v != 0u) - (uint32_t)(best2 != 0u);
-            if (out && v != best2) out[i - pos0] = v;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (V == 9) { const uint64_t u = stamp(); ph[2] += u - tB; tB = u; }
-        qn = 0;
+
+    // Resolve queue.  An item is a depth-3 candidate (qkey = the LE u32
+    // text[i-3..i] = text[i-3] | key24 << 8) or a record step (qpos bit 31; qkey = record | depth
+    // << 23); qpos = position - pos0 (30 bits) | placeholder-nonzero << 30.
+    // Rounds are software-pipelined: issue() loads one set per item (t3h
+    // slot1 + slot2, or the 48-B record + the next stream byte) into the
+    // round registers, and consume() uses them in the next chunk iteration,
+    // so the load latency hides behind a chunk's store, push and LDS work.
+    // Unfinished items go back to the queue for the next round.
+    // The chunk loop is unrolled by two with fixed A/B text windows, so no
+    // loaded register is ever copied (a copy would wait for the load), and
+    // every round issues the same four loads
+    // (idle lanes read a harmless address), so the vmcnt the compiler
+    // computes is static: waiting for a chunk's bytes or for a round never
+    // waits for the younger rounds, stores and prefetches.
+    // Ordering: items of chunk k are issued after chunk k's placeholder
+    // store, and vmcnt retires in order, so a round's results imply the
+    // stores of its items are complete at L2 before any patch overwrites one.
+    struct Round {
+        uint32_t n;  // items (wave-uniform)
+        uint32_t fk, fp, tc;
+        u32x4 L0, L1, L2;
     };
-    // text is prefetched two chunks ahead; streamed bytes and ids are non-temporal
-    int64_t ch = (int64_t)blockIdx.x * RT_WAVES + wid;
-    u32x2 nx[4] = {}, nnx[4] = {};
-    bool nfast = is_fast(ch), nnfast = is_fast(ch + stride);
-    if (nfast) {
-        const uint8_t* src = text + pos0 + ch * RT_CHUNK + 4 * lane - 4;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) nx[s] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(src + 256 * s));
-    }
-    if (nnfast) {
-        const uint8_t* src = text + pos0 + (ch + stride) * RT_CHUNK + 4 * lane - 4;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) nnx[s] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(src + 256 * s));
-    }
-    for (; ch < nchunks; ch += stride) {  // wave-uniform
-        const int64_t pc = pos0 + ch * RT_CHUNK;
-        const bool fast = nfast;
-        const u32x2 x[4] = {nx[0], nx[1], nx[2], nx[3]};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) nx[s] = nnx[s];
-        nfast = nnfast;
-        nnfast = is_fast(ch + 2 * stride);
-        if (nnfast) {  // prefetch two chunks ahead
-            const uint8_t* src = text + pc + 2 * stride * RT_CHUNK + 4 * lane - 4;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) nnx[s] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(src + 256 * s));
+    // The queue is a ring of RT_QCAP items per wave: head qh, count qn.  A
+    // round takes RT_ROUND items from the head once that many are queued
+    // (idle chunks issue an empty round: same four loads, harmless
+    // addresses), so every round runs all 64 lanes.
+    uint32_t qh = 0, qn = 0;  // wave-uniform
+    auto issue = [&](Round& r, uint32_t take) __attribute__((always_inline)) {
+        __builtin_amdgcn_wave_barrier();
+        const bool act = (uint32_t)lane < take;
+        const uint32_t sl = (qh + lane) & (RT_QCAP - 1);
+        r.fk = act ? qkey[sl] : 0u;
+        r.fp = act ? qpos[sl] : 0u;
+        const bool deep = r.fp >> 31;
+        const uint32_t k = r.fk >> 8;
+        const uint32_t node = r.fk & 0x7FFFFFu, d = r.fk >> 23;
+        const int64_t i = pos0 + (int64_t)(r.fp & 0x3FFFFFFFu);
+        const u32x4* R = reinterpret_cast<const u32x4*>(t.rec) + (size_t)node * 3;
+        const u32x4* T = reinterpret_cast<const u32x4*>(t.t3h);
+        const u32x4* a0 = deep ? R : T + rt_slot1(k, t.t3h_bits);
+        const u32x4* a1 = deep ? R + 1 : T + rt_slot2(k, t.t3h_bits);
+        const u32x4* a2 = deep ? R + 2 : reinterpret_cast<const u32x4*>(t.filt);
+        const uint8_t* a3 = (deep && (int64_t)d <= i - stream_start) ? text + (i - d) : dummy;
+        r.L0 = *a0;
+        r.L1 = *a1;
+        r.L2 = *a2;
+        r.tc = *a3;
+        r.n = take;
+        qh += take;
+        qn -= take;
+    };
+    auto consume = [&](Round& r) __attribute__((always_inline)) {
+        // Nothing computed from the round may be hoisted above this point
+        // (the compiler otherwise speculates it up to the loads and waits).
+        // (Fenced copies: the round's own registers are never redefined.)
+        u32x4 L0 = r.L0, L1 = r.L1, L2 = r.L2;
+        uint32_t tc = r.tc, fk = r.fk, fp = r.fp;
+        asm volatile("" : "+v"(L0), "+v"(L1), "+v"(L2), "+v"(tc), "+v"(fk), "+v"(fp)::"memory");
+        if (V == 9) { const uint64_t u = stamp(); ph[2] += u - tB; tB = u; }
+        bool again = false;
+        uint32_t nk = 0, np = 0;
+        if ((uint32_t)lane < r.n) {
+            const int64_t i = pos0 + (int64_t)(fp & 0x3FFFFFFFu);
+            const int64_t avail = i - stream_start + 1;
+            uint32_t v, ph0 = 0xFFFFFFFFu, node = 0, d = 0;  // ph0: the stored placeholder, when known
+            if (!(fp >> 31)) {
+                const uint32_t k = fk >> 8, c3 = fk & 0xFFu;
+                ph0 = s_t[k >> 8] & 0x7FFFu;
+                const uint32_t want = T3H_VALID | k;
+                const bool h0 = (L0.x & 0x1FFFFFFu) == want;
+                const u32x4 e = h0 ? L0 : L1;
+                v = ph0;
+                if ((e.x & 0x1FFFFFFu) == want) {
+                    v = e.y;
+                    const uint32_t kind = e.x >> 25;
+                    if (avail >= 4 && kind == 1) {
+                        const uint32_t nch = e.z >> 24;
+                        const uint32_t j = c3 == (e.z & 0xFFu) ? 0u : c3 == ((e.z >> 8) & 0xFFu) ? 1u
+                                         : c3 == ((e.z >> 16) & 0xFFu) ? 2u : 3u;
+                        if (j < nch) {
+                            if (nch == 1 && !(e.w & CONT32)) {
+                                v = e.w;
+                            } else {
+                                again = true;
+                                node = nch == 1 ? e.w & 0x7FFFFFFFu : e.w + j;
+                                d = 4;
+                            }
+                        }
+                    } else if (avail >= 4 && kind == 2) {
+                        again = true;
+                        node = e.w & 0x7FFFFFFFu;
+                        d = 3;
+                    }
+                }
+            } else {
+                d = fk >> 23;
+                v = L2.y;  // {base, best, prefix lo, prefix hi}
+                if ((int64_t)d < avail) {
+                    const uint32_t w = tc >> 5, bit = tc & 31u;
+                    // bit-test select tree (an equality chain becomes a
+                    // dynamic extract, which lowers through scratch)
+                    const uint32_t s0 = (w & 1) ? L0.y : L0.x, s1 = (w & 1) ? L0.w : L0.z;
+                    const uint32_t s2 = (w & 1) ? L1.y : L1.x, s3 = (w & 1) ? L1.w : L1.z;
+                    const uint32_t s4 = (w & 2) ? s1 : s0, s5 = (w & 2) ? s3 : s2;
+                    const uint32_t word = (w & 4) ? s5 : s4;
+                    if ((word >> bit) & 1u) {
+                        const uint32_t pre = ((w < 4 ? L2.z : L2.w) >> (8 * (w & 3))) & 0xFFu;
+                        node = L2.x + pre + __popc(word & ((1u << bit) - 1u));
+                        ++d;
+                        again = true;
+                    }
+                }
+            }
+            if (again) {
+                nk = node | (d << 23);
+                np = fp | 0x80000000u;
+            } else {
+                cnt += (uint32_t)(v != 0u) - ((fp >> 30) & 1u);
+                if (DENSE && v != ph0) out[i - pos0] = v;
+            }
         }
-        if (!fast) continue;  // stream start / tail: handled after the loop
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t m = __ballot(again);
+        if (again) {
+            const uint32_t sl = (qh + qn + wave_prefix(m)) & (RT_QCAP - 1);
+            qkey[sl] = nk;
+            qpos[sl] = np;
+        }
+        __builtin_amdgcn_wave_barrier();
+        qn += (uint32_t)__popcll(m);
+        r.n = 0;
+    };
+    auto window = [&](int64_t c, int s) __attribute__((always_inline)) -> const u32x2* {
+        const uint8_t* base = c < c_hi ? text + pos0 + c * RT_CHUNK - 4 : dummy - 4;
+        return reinterpret_cast<const u32x2*>(base + 256 * s + 4 * lane);
+    };
+    auto stand_in_store = [&]() __attribute__((always_inline)) {
+        if (DENSE) {
+            uint4* o = reinterpret_cast<uint4*>(t.scratch);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(o + 64 * s + lane));
+        }
+    };
+    Round rr;
+    rr.n = 0;
+    u32x2 xa[4], xb[4];
+    int64_t ch = c_lo + (int64_t)blockIdx.x * RT_WAVES + wid;
+    // One chunk: depth<=2 answers from LDS, filter, the previous chunk's
+    // round consumed and a new one issued, the store,
+    // the push of this chunk's candidates, the prefetch two chunks ahead.
+    auto chunk = [&](u32x2 (&x)[4], int64_t c) __attribute__((always_inline)) {
+        const int64_t pc = pos0 + c * RT_CHUNK;
         if (V == 9) { tB = stamp(); ph[6] += 1; }
         // position j = 4s + b of this lane is pc + 256s + 4*lane + b; its key
         // is the LE u24 ending at byte b of x[s].y (bytes i-2, i-1, i)
 #define RT_KEY(j) ((uint32_t)((((uint64_t)x[(j) >> 2].y << 32) | x[(j) >> 2].x) >> (8 * (2 + ((j) & 3)))) & 0xFFFFFFu)
-        uint32_t r[16];
+        uint32_t res[16];
         uint32_t cm = 0;  // bit j: position j goes past depth 2
 #pragma unroll
-        for (int j = 0; j < 16; ++j) r[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
+        for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
         if (V == 0 || V == 9) {
             uint32_t fw[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) fw[j] = s_f[__umulhi(rt_hash(RT_KEY(j)), (uint32_t)RT_FILTER_WORDS)];
+            for (int j = 0; j < 16; ++j) fw[j] = s_f[rt_fhash(RT_KEY(j)) >> 20];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t m = rt_fmask(rt_hash(RT_KEY(j)));
-                cm |= (((r[j] >> 15) & 1u) & (uint32_t)((fw[j] & m) == m)) << j;
-            }
+            for (int j = 0; j < 16; ++j) cm |= ((res[j] >> 15) & rt_fhit(fw[j], rt_fhash(RT_KEY(j)))) << j;
         }
 #undef RT_KEY
+        uint32_t nzm = 0;  // bit j: placeholder j is nonzero
 #pragma unroll
-        for (int j = 0; j < 16; ++j) r[j] &= 0x7FFFu;
+        for (int j = 0; j < 16; ++j) {
+            res[j] &= 0x7FFFu;
+            nzm |= (uint32_t)(res[j] != 0u) << j;
+        }
+        cnt += __popc(nzm);
         if (V == 9) { const uint64_t u = stamp(); ph[0] += u - tB; tB = u; }
-        // store the chunk: depth<=2 answers, queued positions patched by flush()
-        if (out) {
+        if (V == 0 || V == 9) {
+            if (rr.n) consume(rr);                      // the round issued last chunk
+            if (V == 9) { const uint64_t u = stamp(); ph[3] += u - tB; tB = u; }
+            issue(rr, qn >= RT_ROUND ? RT_ROUND : 0u);  // items of earlier chunks (stores issued)
+            if (V == 9) { const uint64_t u = stamp(); ph[5] += u - tB; tB = u; }
+        }
+        // store the chunk: depth<=2 answers, queued positions patched later
+        if (DENSE) {
             uint4* o = reinterpret_cast<uint4*>(out + (pc - pos0));
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                u32x4 v = {r[4 * s], r[4 * s + 1], r[4 * s + 2], r[4 * s + 3]};
+                u32x4 v = {res[4 * s], res[4 * s + 1], res[4 * s + 2], res[4 * s + 3]};
                 __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o + 64 * s + lane));
             }
         }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) cnt += r[j] != 0u;
         asm volatile("" ::: "memory");  // the store stays ahead of any later probe
         if (V == 9) { const uint64_t u = stamp(); ph[4] += u - tB; tB = u; }
         if (V == 0 || V == 9) {
-            // lane count c = popc(cm); exclusive wave prefix from five ballots
-            // (one per bit of c); items written by a loop over own set bits
+            // lane count c = popc(cm); exclusive wave prefix by a DPP scan;
+            // items written by a loop over the lane's own set bits
             const uint32_t c = __popc(cm);
-            uint32_t base = 0, total = 0;
-#pragma unroll
-            for (int b = 0; b < 5; ++b) {
-                const uint64_t mb = __ballot((c >> b) & 1u);
-                base += wave_prefix(mb) << b;
-                total += (uint32_t)__popcll(mb) << b;
-            }
+            const uint32_t incl = wave_scan_incl(c);
+            const uint32_t base = incl - c;
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
             for (uint32_t done = 0;;) {  // wave-uniform
+                // room for the in-flight rounds' survivors is kept
+                const uint32_t room = RT_QCAP - qn - rr.n;
                 uint32_t mm = cm, rank = base;
-                while (mm) {
+                while (mm) {  // per lane: its own candidates, in position order
                     const uint32_t j = __builtin_ctz(mm);
                     mm &= mm - 1;
-                    const uint32_t slot = qn + rank - done;
-                    if (rank >= done && slot < RT_QCAP) {
+                    if (rank >= done && rank - done < room) {
+                        const uint32_t slot = (qh + qn + rank - done) & (RT_QCAP - 1);
                         const uint32_t sg = j >> 2, b = j & 3;
-                        const uint32_t lo = sg == 0 ? x[0].x : sg == 1 ? x[1].x : sg == 2 ? x[2].x : x[3].x;
-                        const uint32_t hi = sg == 0 ? x[0].y : sg == 1 ? x[1].y : sg == 2 ? x[2].y : x[3].y;
-                        const uint64_t win = ((uint64_t)hi << 32) | lo;
-                        qkey[slot] = ((uint32_t)(win >> (8 * (2 + b))) & 0xFFFFFFu) |
-                                     (((uint32_t)(win >> (8 * (1 + b))) & 0xFFu) << 24);
-                        qpos[slot] = (uint32_t)(pc - pos0) + 256 * sg + 4 * lane + b;
+                        // bit-test select tree (no dynamic register index)
+                        const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
+                        const u32x2 w = (sg & 2) ? w23 : w01;
+                        // text[i-3..i] = window bytes 1+b .. 4+b (alignbit uses
+                        // the shift mod 32, so b = 3 is the high word itself)
+                        qkey[slot] = b == 3 ? w.y : __builtin_amdgcn_alignbit(w.y, w.x, 8 * (1 + b));
+                        qpos[slot] = ((uint32_t)(pc - pos0) + 256 * sg + 4 * lane + b) | (((nzm >> j) & 1u) << 30);
                     }
                     ++rank;
                 }
-                const uint32_t took = (total - done < RT_QCAP - qn) ? total - done : RT_QCAP - qn;
+                const uint32_t took = total - done < room ? total - done : room;
                 qn += took;
                 done += took;
-                if (qn < RT_QFLUSH && done == total) break;
-                flush();
                 if (done == total) break;
+                // queue full (dense matches): resolve synchronously in
+                // separate registers; these waits cover this chunk's stores
+                if (rr.n) {
+                    consume(rr);
+                } else {
+                    Round rs;
+                    issue(rs, qn < RT_ROUND ? qn : RT_ROUND);
+                    consume(rs);
+                }
             }
+            if (V == 9) { const uint64_t u = stamp(); ph[1] += u - tB; tB = u; }
         }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) x[s] = __builtin_nontemporal_load(window(c + 2 * stride, s));
+    };
+    // Enter the loop with the memory-op pattern of the steady state (round,
+    // store, prefetch; round, store, prefetch) so the compiler's vmcnt is the
+    // steady-state one.
+    Round r0;
+    if (V == 0 || V == 9) issue(r0, 0);
+    stand_in_store();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xa[s] = __builtin_nontemporal_load(window(ch, s));
+    if (V == 0 || V == 9) issue(rr, 0);
+    stand_in_store();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xb[s] = __builtin_nontemporal_load(window(ch + stride, s));
+    for (;;) {  // wave-uniform
+        if (ch >= c_hi) break;
+        chunk(xa, ch);
+        if (ch + stride >= c_hi) break;
+        chunk(xb, ch + stride);
+        ch += 2 * stride;
     }
     if (V == 0 || V == 9) {
-        if (qn) flush();
+        if (rr.n) consume(rr);
+        while (qn) {  // wave-uniform; every round advances each item
+            Round rs;
+            issue(rs, qn < RT_ROUND ? qn : RT_ROUND);
+            consume(rs);
+        }
     }
     if (V == 9) {
         ph[7] = stamp() - tA;
@@ -292,19 +461,23 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         return;
     }
     // the (at most two) chunks that touch the stream start or the tail, one
-    // position at a time; kept out of the main loop to keep it lean
-    for (int64_t c = (int64_t)blockIdx.x * RT_WAVES + wid; c < nchunks; c += stride) {
-        if (is_fast(c)) continue;
-        const int64_t pc = pos0 + c * RT_CHUNK;
+    // position at a time, by two waves of the last workgroup
+    if (blockIdx.x == gridDim.x - 1 && wid < 2) {
+        int64_t c = -1;
+        if (wid == 0 && c_lo == 1) c = 0;
+        if (wid == 1 && c_hi < nchunks && !(c_lo == 1 && c_hi == 0)) c = c_hi;
+        if (c >= 0) {
+            const int64_t pc = pos0 + c * RT_CHUNK;
 #pragma unroll 1
-        for (int s = 0; s < 4; ++s) {
-            const int64_t p = pc + 256 * s + 4 * lane;
+            for (int s = 0; s < 4; ++s) {
+                const int64_t p = pc + 256 * s + 4 * lane;
 #pragma unroll 1
-            for (int b = 0; b < 4; ++b) {
-                if (p + b < pos0 + n) {
-                    const uint32_t v = rt_one(text, s_t, t, p + b, stream_start);
-                    if (out) out[p + b - pos0] = v;
-                    cnt += v != 0u;
+                for (int b = 0; b < 4; ++b) {
+                    if (p + b < pos0 + n) {
+                        const uint32_t v = rt_one(text, s_t, t, p + b, stream_start);
+                        if (DENSE) out[p + b - pos0] = v;
+                        cnt += v != 0u;
+                    }
                 }
             }
         }
@@ -376,8 +549,8 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
                                  uint32_t* out, unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s,
                                  int blocks_override) {
     if (n <= 0) return hipSuccess;
-    // queued positions are kept as u32 offsets from pos0: split huge scans
-    constexpr int64_t PIECE = (int64_t)1 << 31;
+    // queued positions are kept as 30-bit offsets from pos0: split huge scans
+    constexpr int64_t PIECE = (int64_t)1 << 30;
     if (n > PIECE) {
         for (int64_t off = 0; off < n; off += PIECE) {
             const int64_t m = n - off < PIECE ? n - off : PIECE;
@@ -392,12 +565,20 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
     if (blocks > num_cu) blocks = num_cu;  // persistent: one 1024-lane workgroup per CU (LDS-bound)
     if (blocks_override > 0) blocks = blocks_override;
     const dim3 g((unsigned)blocks), b(RT_THREADS);
+#define RT_LAUNCH(VV)                                                                                        \
+    do {                                                                                                     \
+        if (out)                                                                                             \
+            hipLaunchKernelGGL((rt_scan_kernel<VV, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
+        else                                                                                                 \
+            hipLaunchKernelGGL((rt_scan_kernel<VV, false>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
+    } while (0)
     switch (variant) {
-        case 1: hipLaunchKernelGGL(rt_scan_kernel<1>, g, b, 0, s, text, stream_start, pos0, n, out, count, t); break;
-        case 2: hipLaunchKernelGGL(rt_scan_kernel<2>, g, b, 0, s, text, stream_start, pos0, n, out, count, t); break;
-        case 9: hipLaunchKernelGGL(rt_scan_kernel<9>, g, b, 0, s, text, stream_start, pos0, n, out, count, t); break;
-        default: hipLaunchKernelGGL(rt_scan_kernel<0>, g, b, 0, s, text, stream_start, pos0, n, out, count, t);
+        case 1: RT_LAUNCH(1); break;
+        case 2: RT_LAUNCH(2); break;
+        case 9: RT_LAUNCH(9); break;
+        default: RT_LAUNCH(0);
     }
+#undef RT_LAUNCH
     return hipGetLastError();
 }
 

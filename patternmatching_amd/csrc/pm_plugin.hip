@@ -207,6 +207,8 @@ void pm_hip_compile(void* obj) {
             o->rt.t3h = (const uint4*)dalloc_copy(o, im.t3h.data(), im.t3h.size() * 4);
             o->rt.t3h_bits = im.t3h_bits;
             o->rt.rec = (const uint32_t*)dalloc_copy(o, im.rec.data(), im.rec.size() * 4);
+            const std::vector<uint8_t> zero(RT_SCRATCH_BYTES, 0);
+            o->rt.scratch = (uint32_t*)dalloc_copy(o, zero.data(), zero.size());
         } else {
             std::fprintf(stderr, "pm_hip: dictionary exceeds the reverse-trie u16 encoding; using the DFA kernel\n");
             o->kind = KIND_AC;

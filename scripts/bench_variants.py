@@ -56,8 +56,8 @@ if "9" in args.variants.split(","):
                                       cnt.data_ptr(), s.cuda_stream, 0)
         torch.cuda.synchronize()
         c = [int(x) for x in cnt.tolist()]
-        names = ["lds_filter", "push", "resolve", "pull", "store", "rounds", "chunks", "total"]
-        res[f"v9-stamps-{mode}"] = {k: (c[i] / c[6] if i < 5 or i == 7 else c[i]) for i, k in enumerate(names)}
+        names = ["lds_filter", "push", "round_wait", "consume", "store", "issue", "chunks", "total"]
+        res[f"v9-stamps-{mode}"] = {k: (c[i] / c[6] if i != 6 else c[i]) for i, k in enumerate(names)}
 for v in (7, 8):
     if str(v) in args.variants.split(","):
         cnt.zero_()

@@ -36,32 +36,33 @@ class FlatImage:
             self.lib.pm_flat_free(self.h)
 
 
-FILTER_WORDS = 6144
+FILTER_WORDS = 4096
 
 
 def rt_hash(k):
-    """pm_rt_hash: key24 * 0x9E3779B1 mod 2^32."""
+    """pm_rt_hash: key24 * 0x9E3779B1 mod 2^32 (t3h slots)."""
     return (np.asarray(k).astype(np.uint64) * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)
 
 
 def filter_maybe(filt, key24):
-    h = rt_hash(key24)
-    w = filt[((h * np.uint64(FILTER_WORDS)) >> np.uint64(32)).astype(np.int64)].astype(np.uint64)
-    m = (np.uint64(1) << ((h >> np.uint64(4)) & np.uint64(31))) | (np.uint64(1) << ((h >> np.uint64(9)) & np.uint64(31)))
+    """pm_rt_fhash / pm_rt_filter_word / pm_rt_filter_mask: 3 bits per key."""
+    f = (np.asarray(key24).astype(np.uint64) * np.uint64(0x9E3779)) & np.uint64(0xFFFFFFFF)
+    w = filt[(f >> np.uint64(20)).astype(np.int64)].astype(np.uint64)
+    m = np.zeros_like(f)
+    for sh in (5, 10, 15):
+        m |= np.uint64(1) << ((f >> np.uint64(sh)) & np.uint64(31))
     return (w & m) == m
 
 
 def t3h_lookup(t3h, bits, key24):
-    """The 4-word entry of key24, or None."""
-    mask = (1 << bits) - 1
-    slot = int(rt_hash(np.array([key24], np.uint32))[0]) >> (32 - bits)
-    while True:
+    """The 4-word entry of key24 (cuckoo: slot1 or slot2), or None."""
+    s1 = int(rt_hash(np.array([key24], np.uint32))[0]) >> (32 - bits)
+    s2 = ((key24 * 0x85EBCA77) & 0xFFFFFFFF) >> (32 - bits)
+    for slot in (s1, s2):
         e = t3h[4 * slot:4 * slot + 4]
-        if not int(e[0]) & (1 << 24):
-            return None
-        if int(e[0]) & 0xFFFFFF == key24:
+        if int(e[0]) & 0x1FFFFFF == (1 << 24) | key24:
             return [int(x) for x in e]
-        slot = (slot + 1) & mask
+    return None
 
 
 def rec_walk(rec, text, p, avail, node, d):
@@ -107,8 +108,13 @@ def rt_scan(img, text, stream_start=0, use_filter=True):
         if kind == 0 or avail[p] < 4:
             out[p] = e[1]
         elif kind == 1:
-            if int(text[p - 3]) != e[2]:
+            nch = e[2] >> 24
+            kids = [(e[2] >> (8 * k)) & 0xFF for k in range(nch)]
+            c3 = int(text[p - 3])
+            if c3 not in kids:
                 out[p] = e[1]
+            elif nch > 1:
+                out[p] = rec_walk(rec, text, p, avail[p], e[3] + kids.index(c3), 4)
             elif not e[3] & 0x80000000:
                 out[p] = e[3]
             else:
