@@ -29,6 +29,7 @@ METRIC = "GB/s stream scanned + matches/sec, snort.dict, 1/2/4/8 MI355X vs CPU r
 DATA = os.path.join(REPO, "tests", "golden", "data")
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
+WIDTH = {"dense": 4, "dense16": 2, "count": 0}  # bytes written per stream position
 
 
 def parse():
@@ -38,7 +39,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--dict", default="snort", choices=list(DICTS))
     p.add_argument("--bytes", type=int, default=1 << 30, help="stream bytes per GPU")
-    p.add_argument("--mode", default="dense", choices=["dense", "count"])
+    p.add_argument("--mode", default="dense", choices=list(WIDTH),
+                   help="dense: u32 id per position; dense16: u16 id per position; count: match count only")
     p.add_argument("--kernel", default="rt", choices=["rt", "ac"])
     p.add_argument("--stream", default="ascii", choices=["ascii", "bytes"])
     p.add_argument("--seed", type=int, default=1)
@@ -120,12 +122,13 @@ def main():
     if lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, seed, 0 if args.stream == "ascii" else 1,
                                     stream.cuda_stream) != 0:
         raise RuntimeError(lib.pm_hip_last_error().decode())
-    out = torch.empty(n, dtype=torch.int32, device="cuda") if args.mode == "dense" else None
+    width = WIDTH[args.mode]
+    out = torch.empty(n, dtype={4: torch.int32, 2: torch.int16}[width], device="cuda") if width else None
     count = torch.zeros(1, dtype=torch.int64, device="cuda")
     out_ptr = out.data_ptr() if out is not None else None
 
     def step():
-        m.scan_device(text.data_ptr(), 0, 0, n, out_ptr, count.data_ptr(), stream.cuda_stream)
+        m.scan_device(text.data_ptr(), 0, 0, n, out_ptr, count.data_ptr(), stream.cuda_stream, out_width=width or 4)
 
     for _ in range(args.warmup):
         step()
@@ -158,7 +161,7 @@ def main():
     if rank == 0:
         total_bytes = world * n * args.steps
         value = total_bytes / elapsed / 1e9
-        alg_per_pos = 5 if args.mode == "dense" else 1  # 1 B read + 4 B id written (dense)
+        alg_per_pos = 1 + width  # 1 B read + the id written per position
         achieved = n * alg_per_pos / (kernel_ms * 1e-3) / 1e9
         workload_key = f"{args.dict}-{args.stream}-{n}-{args.mode}-{args.kernel}"
         tr = load_traffic(workload_key)
@@ -179,7 +182,8 @@ def main():
                     "dictionaries from the reference" % args.stream,
             "config": {
                 "workload": f"{args.dict}.dict, {n} B {args.stream} stream per GPU, "
-                            f"{'dense u32 match id per position' if args.mode == 'dense' else 'match count only'}",
+                            + {"dense": "dense u32 match id per position", "dense16": "dense u16 match id per position",
+                               "count": "match count only"}[args.mode],
                 "dict": args.dict,
                 "stream_bytes_per_gpu": n,
                 "mode": args.mode,

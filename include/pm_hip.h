@@ -78,6 +78,12 @@ int pm_hip_read_block_gid(void* obj, const uint8_t* buf, size_t n, uint32_t* out
  */
 int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0,
                        int64_t n, uint32_t* d_out, unsigned long long* d_count, void* hip_stream);
+/* The same with u16 gids (n * 2 bytes, 16-byte aligned): the compact id
+ * stream for dictionaries of fewer than 65536 patterns (every reference
+ * dictionary; the merged snort + ET set has 55,580).  Returns -4 when the
+ * dictionary is larger. */
+int pm_hip_scan_device16(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0,
+                         int64_t n, uint16_t* d_out, unsigned long long* d_count, void* hip_stream);
 
 /* Device-side synthetic stream, identical to pm_gen_stream_host(). */
 int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
@@ -102,11 +108,12 @@ int pm_hip_device_count(void);
 int pm_hip_set_device(int device);
 
 /* Timing-only ablation launches of the reverse-trie kernel (variant 0 =
- * product kernel, 1 = no depth>=3 stage, 2 = streaming only, 3 = no LDS
- * filter); blocks <= 0
- * keeps the default grid.  Outputs of variants 1-2 are not match ids. */
-int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, uint32_t* d_out,
-                              unsigned long long* d_count, void* hip_stream, int blocks);
+ * product kernel, 1 = no depth>=3 stage, 2 = streaming only, 9 = product
+ * kernel with per-phase cycle stamps summed into d_count[0..7]); out_width
+ * 4 / 2 = u32 / u16 ids (d_out may be NULL: count only); blocks <= 0 keeps
+ * the default grid.  Outputs of variants 1-2 are not match ids. */
+int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out,
+                              int out_width, unsigned long long* d_count, void* hip_stream, int blocks);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpm.so")
+# PM_LIBPM: an alternative build of the same library, for side-by-side
+# timing of kernel revisions in one process tree (scripts/ab_time.sh).
+LIB_PATH = os.environ.get("PM_LIBPM") or os.path.join(_HERE, "libpm.so")
 CLI_PATH = os.path.join(_HERE, "bin", "pm")
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -82,6 +84,8 @@ SIGNATURES = {
     "pm_hip_read_block_gid": (ctypes.c_int, [c_vp, c_u8p, ctypes.c_size_t, c_u32p]),
     "pm_hip_scan_device": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, c_vp,
                                           c_vp, c_vp]),
+    "pm_hip_scan_device16": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, c_vp,
+                                            c_vp, c_vp]),
     "pm_hip_gen_stream_device": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_int, c_vp]),
     "pm_gen_stream_host": (None, [c_u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
@@ -94,8 +98,8 @@ SIGNATURES = {
     "pm_hip_last_error": (ctypes.c_char_p, []),
     "pm_hip_device_count": (ctypes.c_int, []),
     "pm_hip_set_device": (ctypes.c_int, [ctypes.c_int]),
-    "pm_hip_debug_scan_variant": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int64, c_vp, c_vp, c_vp,
-                                                 ctypes.c_int]),
+    "pm_hip_debug_scan_variant": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int64, c_vp, ctypes.c_int,
+                                                 c_vp, c_vp, ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
     "pm_flat_fits": (ctypes.c_int, [c_vp]),

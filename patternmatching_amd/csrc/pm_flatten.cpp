@@ -150,7 +150,8 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
     uint32_t d3 = 0;
     for (uint32_t v = 1; v < t.n && t.depth[v] <= 2; ++v)
         if (t.depth[v] == 2) d3 += t.ccount[v];
-    im.filt.assign(RT_FILTER_WORDS, 0);
+    im.filt.assign(RT_FILTER_WORDS + RT_F2_WORDS, 0);
+    uint32_t* f2 = &im.filt[RT_FILTER_WORDS];
     auto answer = [&](uint32_t v) { return t.ccount[v] ? (RT_CONT32 | (v - first_d3)) : best[v]; };
     std::vector<std::array<uint32_t, 4>> ents;
     ents.reserve(d3);
@@ -163,6 +164,14 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
             const uint32_t key = c2 | (c1 << 8) | (c0 << 16);
             const uint32_t f = pm_rt_fhash(key);
             im.filt[pm_rt_filter_word(f)] |= pm_rt_filter_mask(f);
+            if (t.gid[n3]) {  // a 3-byte pattern
+                const uint32_t g = pm_rt_p3hash(key);
+                f2[pm_rt_p3word(g)] |= pm_rt_filter_mask(g);
+            }
+            for (uint32_t q = 0; q < t.ccount[n3]; ++q) {  // depth-4 suffixes
+                const uint32_t g = pm_rt_s4hash(t.label[t.cstart[n3] + q] | (key << 8));
+                f2[pm_rt_s4word(g)] |= pm_rt_filter_mask(g);
+            }
             std::array<uint32_t, 4> e{};
             const uint32_t nch = t.ccount[n3];
             const uint32_t kind = nch == 0 ? 0u : (nch <= RT_T3H_INLINE ? 1u : 2u);
@@ -181,7 +190,8 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
         }
     }
     im.d3 = (uint32_t)ents.size();
-    for (im.t3h_bits = 4; (1u << im.t3h_bits) < 2 * im.d3; ++im.t3h_bits) {}
+    // load <= 1/4: few keys need their slot2 (the device probes slot1 first)
+    for (im.t3h_bits = 4; (1u << im.t3h_bits) < 4 * im.d3; ++im.t3h_bits) {}
     for (;; ++im.t3h_bits) {  // load <= 1/2: two-choice cuckoo insertion virtually never fails; grow if it does
         const uint32_t bits = im.t3h_bits;
         im.t3h.assign((size_t)4 << bits, 0);

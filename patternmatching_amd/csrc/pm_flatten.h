@@ -10,11 +10,19 @@
 //             t12   u16[65536 + 256]  depth<=2 in one lookup (first 64K
 //                                     LDS-resident): best pattern so far, bit
 //                                     15 set when the depth-2 node has children
-//             filt  u32[RT_FILTER_WORDS] blocked Bloom filter (3 bits per key)
-//                                     of the 3-byte suffixes that are depth-3
-//                                     nodes (LDS-resident): no false negatives
+//             filt  u32[RT_FILTER_WORDS + RT_F2_WORDS], LDS-resident:
+//                   stage 1: blocked Bloom filter (3 bits per key) of the
+//                     3-byte suffixes that are depth-3 nodes (every
+//                     position under a depth-2 node with children tests it);
+//                   stage 2 (only queued stage-1 candidates test it): the
+//                     3-byte suffixes that are patterns (RT_F3_WORDS) and
+//                     the 4-byte suffixes that are depth-4 nodes
+//                     (RT_F4_WORDS).  A position failing stage 2 has no
+//                     pattern at depth >= 3 on its walk, so its answer is
+//                     the depth-2 one and it needs no probe.
+//                   No false negatives in either stage.
 //             t3h   u32x4[2^k]        open-addressing table of those suffixes
-//                                     (two-choice cuckoo, load <= 1/2), one 16-B entry per
+//                                     (two-choice cuckoo, load <= 1/4), one 16-B entry per
 //                                     depth-3 node n3 that decides depth 4 too:
 //                                       x = kind << 25 | valid << 24 | key24
 //                                           (kind 0: n3 has no children,
@@ -80,20 +88,31 @@ constexpr uint32_t RT_T1_BASE = 65536;   // t12[65536 + c]: lookback of exactly 
 constexpr uint32_t RT_CONT16 = 0x8000u;  // t12: depth-2 node has children (low 15 bits: best so far)
 constexpr uint32_t RT_CONT32 = 0x80000000u;  // t3: continue at record (low 31 bits)
 constexpr int RT_REC_WORDS = 12;
-constexpr uint32_t RT_FILTER_WORDS = 4096;  // 16 KiB of LDS
+constexpr uint32_t RT_FILTER_WORDS = 4096;  // stage 1: 16 KiB of LDS
+constexpr uint32_t RT_F3_WORDS = 256;       // stage 2, 3-byte patterns: 1 KiB
+constexpr uint32_t RT_F4_WORDS = 1792;      // stage 2, depth-4 suffixes: 7 KiB
+constexpr uint32_t RT_F2_WORDS = RT_F3_WORDS + RT_F4_WORDS;
 
 // Hashes (host and device must agree).  key24 = text[i-2] | text[i-1] << 8
 // | text[i] << 16 (the little-endian u24 ending at i, so the t12 index is
 // key24 >> 8).  Filter: f = key24 * 0x9E3779 (mod 2^32; one full-rate 24-bit
-// multiply on the device), word f >> 20, bits (f >> 5), (f >> 10) and
-// (f >> 15) (& 31).  t3h: a key sits in slot pm_rt_slot1 (h >> (32 -
+// multiply on the device), word f >> 20, bits f, f >> 8 and f >> 16 (& 31:
+// byte fields, so the device shifts take them by SDWA byte select).  t3h: a key sits in slot pm_rt_slot1 (h >> (32 -
 // t3h_bits), h = key24 * 0x9E3779B1) or pm_rt_slot2.
 inline uint32_t pm_rt_hash(uint32_t k) { return k * 0x9E3779B1u; }
 inline uint32_t pm_rt_fhash(uint32_t k) { return k * 0x9E3779u; }
 inline uint32_t pm_rt_filter_word(uint32_t f) { return f >> 20; }
 inline uint32_t pm_rt_filter_mask(uint32_t f) {
-    return (1u << ((f >> 5) & 31)) | (1u << ((f >> 10) & 31)) | (1u << ((f >> 15) & 31));
+    return (1u << (f & 31)) | (1u << ((f >> 8) & 31)) | (1u << ((f >> 16) & 31));
 }
+// Stage 2 (word indices relative to the stage-2 block, same bit mask):
+// 3-byte patterns g = key24 * 0x85EBCA, word g >> 24; depth-4 suffixes
+// g = key32 * 0x9E3779B1 with key32 = text[i-3] | key24 << 8, word
+// RT_F3_WORDS + ((g >> 20) * 7 >> 4).
+inline uint32_t pm_rt_p3hash(uint32_t key24) { return key24 * 0x85EBCAu; }
+inline uint32_t pm_rt_p3word(uint32_t g) { return g >> 24; }
+inline uint32_t pm_rt_s4hash(uint32_t key32) { return key32 * 0x9E3779B1u; }
+inline uint32_t pm_rt_s4word(uint32_t g) { return RT_F3_WORDS + (((g >> 20) * 7u) >> 4); }
 constexpr uint32_t RT_T3H_VALID = 1u << 24;
 inline uint32_t pm_rt_slot1(uint32_t k, uint32_t bits) { return pm_rt_hash(k) >> (32 - bits); }
 inline uint32_t pm_rt_slot2(uint32_t k, uint32_t bits) { return (k * 0x85EBCA77u) >> (32 - bits); }

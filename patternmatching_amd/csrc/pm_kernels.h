@@ -21,13 +21,14 @@ struct DfaDev {
 };
 
 // Positions [pos0, pos0+n) of text; bytes back to stream_start are context.
-// pos0 % 16 == 0; out (n u32) may be null; count (u64) may be null.
-hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
+// pos0 % 16 == 0.  out: n ids of outw bytes each (4 = u32 gids, 2 = u16
+// gids, valid when every gid < 65536), or null; count (u64) may be null.
+hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                         unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s);
 // ablation variants of the RT kernel (timing only; see pm_kernels.hip)
 hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
-                                uint32_t* out, unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s,
-                                int blocks_override);
-hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
+                                void* out, int outw, unsigned long long* count, const RtDev& t, int num_cu,
+                                hipStream_t s, int blocks_override);
+hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s);
 hipError_t pm_launch_gen(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode, hipStream_t s);

@@ -35,12 +35,16 @@ constexpr int RT_THREADS = 1024;
 constexpr int RT_WAVES = RT_THREADS / 64;
 constexpr int RT_T2_U16 = 65536;
 constexpr int RT_FILTER_WORDS = 4096;  // must match pm_flatten.h
-constexpr uint32_t RT_QCAP = 128;       // queue ring per wave (power of two)
-constexpr uint32_t RT_ROUND = 64;       // items per round (one per lane)
+constexpr int RT_F3_WORDS = 256;        // stage-2 filter words, must match pm_flatten.h
+constexpr int RT_F2_WORDS = 2048;
+constexpr uint32_t RT_QCAP = 64;        // queue ring per wave (power of two, <= 64: one item per lane)
+constexpr uint32_t RT_ROUND = 48;       // a round is issued once this many are queued
 constexpr int RT_CHUNK = 1024;         // positions per wave iteration
 constexpr uint32_t CONT16 = 0x8000u;
 constexpr uint32_t CONT32 = 0x80000000u;
 constexpr uint32_t T3H_VALID = 1u << 24;
+constexpr uint32_t RT_POSMASK = (1u << 30) - 1;  // queue item: position - pos0
+constexpr uint32_t RT_SLOT2 = 1u << 30;          // queue item: probe t3h slot2
 
 __device__ __forceinline__ uint32_t rt_hash(uint32_t k) { return k * 0x9E3779B1u; }  // pm_rt_hash
 // pm_rt_fhash: k < 2^24, so this is one full-rate v_mul_u32_u24 (written
@@ -51,9 +55,16 @@ __device__ __forceinline__ uint32_t rt_fhash(uint32_t k) {
     asm("v_mul_u32_u24 %0, 0x9e3779, %1" : "=v"(h) : "v"(k));
     return h;
 }
-// the three filter bits of f present in word w (shift amounts use bits 0-4)
+// the three filter bits of f (pm_rt_filter_mask) present in word w: shifts
+// by bytes 0, 1, 2 of f (a shift uses bits 0-4 of its amount)
 __device__ __forceinline__ uint32_t rt_fhit(uint32_t w, uint32_t f) {
-    return (w >> ((f >> 5) & 31)) & (w >> ((f >> 10) & 31)) & (w >> ((f >> 15) & 31)) & 1u;
+    uint32_t a, b, c;  // written out: the compiler extracts the bytes with extra shifts
+    asm("v_lshrrev_b32_e32 %0, %1, %2" : "=v"(a) : "v"(f), "v"(w));
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+        : "=v"(b) : "v"(f), "v"(w));
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+        : "=v"(c) : "v"(f), "v"(w));
+    return a & b & c & 1u;
 }
 
 __device__ __forceinline__ uint64_t stamp() {
@@ -63,6 +74,22 @@ __device__ __forceinline__ uint64_t stamp() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
+
+// Stage 2 of the filter for q = text[i-3..i] (pm_rt_p3hash / pm_rt_s4hash):
+// nonzero when key24 = q >> 8 may be a 3-byte pattern or q a depth-4 suffix.
+// Split in two so the LDS reads can be issued well before the test.
+struct Stage2 {
+    uint32_t g3, g4, w3, w4;
+};
+__device__ __forceinline__ Stage2 rt_stage2_load(const uint32_t* s_f2, uint32_t q) {
+    Stage2 z;
+    asm("v_mul_u32_u24 %0, 0x85ebca, %1" : "=v"(z.g3) : "v"(q >> 8));
+    z.g4 = q * 0x9E3779B1u;
+    z.w3 = s_f2[z.g3 >> 24];
+    z.w4 = s_f2[RT_F3_WORDS + (((z.g4 >> 20) * 7u) >> 4)];
+    return z;
+}
+__device__ __forceinline__ uint32_t rt_stage2_hit(const Stage2& z) { return rt_fhit(z.w3, z.g3) | rt_fhit(z.w4, z.g4); }
 
 // Inclusive prefix sum over the 64 lanes: row_shr 1/2/4/8 within rows of 16,
 // then row_bcast 15 / 31 across rows (lanes without a source add 0).
@@ -144,17 +171,30 @@ __device__ uint32_t rt_one(const uint8_t* __restrict__ text, const uint16_t* s_t
 // V (ablation, timing only; V=0 is the product kernel):
 //   1 = loads + t12 lookups + stores (no filter, no queue)
 //   2 = loads + stores only (streaming floor of this access pattern)
+//   3 = 2 plus a sleep per chunk, 4 = 2 plus ~500 dependent VALU per chunk
+//       (how the streaming rate tolerates per-chunk compute)
+//   5 = product kernel whose round loads all hit one line, 6 = product
+//       kernel without patch stores (both: wrong ids, timing only)
+//  10 = product kernel with sc1 (L2-dropping) chunk stores
 //   9 = product kernel with s_memtime stamps per phase (diagnostic: count
 //       receives 8 u64 cycle sums: lds+filter, push, round wait, consume,
 //       store, issue, chunks, total)
-// DENSE: write the per-position ids (read_block); else count only.
-template <int V, bool DENSE>
+// OUTW: bytes per written id: 4 (u32 gids, read_block), 2 (u16 gids, when
+// every gid < 65536), 0 (count only).
+template <int OUTW>
+__device__ __forceinline__ void put_id(void* out, int64_t k, uint32_t v) {
+    if (OUTW == 4) reinterpret_cast<uint32_t*>(out)[k] = v;
+    if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[k] = (uint16_t)v;
+}
+
+template <int V, int OUTW>
 __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
-                                                             int64_t pos0, int64_t n, uint32_t* __restrict__ out,
+                                                             int64_t pos0, int64_t n, void* __restrict__ out,
                                                              unsigned long long* __restrict__ count, RtDev t) {
     __shared__ __attribute__((aligned(16))) uint16_t s_t[RT_T2_U16];
     __shared__ __attribute__((aligned(16))) uint32_t s_f[RT_FILTER_WORDS];
-    __shared__ uint32_t s_qkey[RT_WAVES][RT_QCAP];  // 16 + 16 + 128 KiB: all of the CU's LDS
+    __shared__ __attribute__((aligned(16))) uint32_t s_f2[RT_F2_WORDS];
+    __shared__ uint32_t s_qkey[RT_WAVES][RT_QCAP];  // 128 + 16 + 8 + 8 KiB: all of the CU's LDS
     __shared__ uint32_t s_qpos[RT_WAVES][RT_QCAP];
     {
         const uint4* src = reinterpret_cast<const uint4*>(t.t12);
@@ -163,6 +203,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         const uint4* fsrc = reinterpret_cast<const uint4*>(t.filt);
         uint4* fdst = reinterpret_cast<uint4*>(s_f);
         for (int k = threadIdx.x; k < RT_FILTER_WORDS / 4; k += RT_THREADS) fdst[k] = fsrc[k];
+        uint4* f2dst = reinterpret_cast<uint4*>(s_f2);
+        for (int k = threadIdx.x; k < RT_F2_WORDS / 4; k += RT_THREADS) f2dst[k] = fsrc[RT_FILTER_WORDS / 4 + k];
     }
     __syncthreads();
 
@@ -188,10 +230,18 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
 
     // Resolve queue.  An item is a depth-3 candidate (qkey = the LE u32
-    // text[i-3..i] = text[i-3] | key24 << 8) or a record step (qpos bit 31; qkey = record | depth
-    // << 23); qpos = position - pos0 (30 bits) | placeholder-nonzero << 30.
-    // Rounds are software-pipelined: issue() loads one set per item (t3h
-    // slot1 + slot2, or the 48-B record + the next stream byte) into the
+    // text[i-3..i] = text[i-3] | key24 << 8) or a record step (qpos bit 31;
+    // qkey = record | depth << 23); qpos = position - pos0 (30 bits) |
+    // probe-slot2 << 30.  The match count is settled when a candidate
+    // resolves or turns into record steps (its placeholder is the t12 entry
+    // of its key, recomputed then).  A candidate probes t3h
+    // slot1 only: the key there resolves it, and so does an empty slot1
+    // (cuckoo entries are only ever swapped, so a key whose slot1 is empty
+    // is absent); only a slot1 holding another key sends it to slot2 next
+    // round.  So a round has one scattered load per item (the other three
+    // are scattered only over record steps, a few lanes).
+    // Rounds are software-pipelined: issue() loads one set per item (a t3h
+    // slot, or the 48-B record + the next stream byte) into the
     // round registers, and consume() uses them in the next chunk iteration,
     // so the load latency hides behind a chunk's store, push and LDS work.
     // Unfinished items go back to the queue for the next round.
@@ -205,12 +255,14 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // store, and vmcnt retires in order, so a round's results imply the
     // stores of its items are complete at L2 before any patch overwrites one.
     struct Round {
-        uint32_t n;  // items (wave-uniform)
+        uint32_t n;     // items (wave-uniform)
+        uint32_t keep;  // items that may survive the round (wave-uniform): ring room they hold
         uint32_t fk, fp, tc;
+        uint32_t skip;  // stage 2 rejected the item: its answer is the placeholder
         u32x4 L0, L1, L2;
     };
     // The queue is a ring of RT_QCAP items per wave: head qh, count qn.  A
-    // round takes RT_ROUND items from the head once that many are queued
+    // round takes all queued items once RT_ROUND are queued
     // (idle chunks issue an empty round: same four loads, harmless
     // addresses), so every round runs all 64 lanes.
     uint32_t qh = 0, qn = 0;  // wave-uniform
@@ -221,15 +273,30 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         r.fk = act ? qkey[sl] : 0u;
         r.fp = act ? qpos[sl] : 0u;
         const bool deep = r.fp >> 31;
+        // stage 2 on first probes: only a 3-byte pattern or a depth-4 suffix
+        // can change the placeholder, anything else needs no probe
+        bool skip = false;
+        if (take) {  // wave-uniform
+            const bool first = act && !deep && !(r.fp & RT_SLOT2);
+            if (first) skip = rt_stage2_hit(rt_stage2_load(s_f2, r.fk)) == 0u;
+        }
+        r.skip = skip;
+        r.keep = (uint32_t)__popcll(__ballot(act && !skip));
         const uint32_t k = r.fk >> 8;
         const uint32_t node = r.fk & 0x7FFFFFu, d = r.fk >> 23;
-        const int64_t i = pos0 + (int64_t)(r.fp & 0x3FFFFFFFu);
+        const int64_t i = pos0 + (int64_t)(r.fp & RT_POSMASK);
         const u32x4* R = reinterpret_cast<const u32x4*>(t.rec) + (size_t)node * 3;
         const u32x4* T = reinterpret_cast<const u32x4*>(t.t3h);
-        const u32x4* a0 = deep ? R : T + rt_slot1(k, t.t3h_bits);
-        const u32x4* a1 = deep ? R + 1 : T + rt_slot2(k, t.t3h_bits);
-        const u32x4* a2 = deep ? R + 2 : reinterpret_cast<const u32x4*>(t.filt);
+        const u32x4* F = reinterpret_cast<const u32x4*>(t.filt);  // a harmless line
+        const uint32_t slot = (r.fp & RT_SLOT2) ? rt_slot2(k, t.t3h_bits) : rt_slot1(k, t.t3h_bits);
+        const u32x4* a0 = deep ? R : (skip ? F : T + slot);
+        const u32x4* a1 = deep ? R + 1 : F;
+        const u32x4* a2 = deep ? R + 2 : F;
         const uint8_t* a3 = (deep && (int64_t)d <= i - stream_start) ? text + (i - d) : dummy;
+        if (V == 5) {  // ablation: every round load hits one line (results wrong)
+            a0 = a1 = a2 = F;
+            a3 = dummy;
+        }
         r.L0 = *a0;
         r.L1 = *a1;
         r.L2 = *a2;
@@ -248,18 +315,21 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         if (V == 9) { const uint64_t u = stamp(); ph[2] += u - tB; tB = u; }
         bool again = false;
         uint32_t nk = 0, np = 0;
-        if ((uint32_t)lane < r.n) {
-            const int64_t i = pos0 + (int64_t)(fp & 0x3FFFFFFFu);
+        if ((uint32_t)lane < r.n && !r.skip) {
+            const int64_t i = pos0 + (int64_t)(fp & RT_POSMASK);
             const int64_t avail = i - stream_start + 1;
             uint32_t v, ph0 = 0xFFFFFFFFu, node = 0, d = 0;  // ph0: the stored placeholder, when known
+            bool reprobe = false;
             if (!(fp >> 31)) {
                 const uint32_t k = fk >> 8, c3 = fk & 0xFFu;
                 ph0 = s_t[k >> 8] & 0x7FFFu;
                 const uint32_t want = T3H_VALID | k;
-                const bool h0 = (L0.x & 0x1FFFFFFu) == want;
-                const u32x4 e = h0 ? L0 : L1;
+                const u32x4 e = L0;
                 v = ph0;
-                if ((e.x & 0x1FFFFFFu) == want) {
+                if ((e.x & 0x1FFFFFFu) != want && (e.x & T3H_VALID) && !(fp & RT_SLOT2)) {
+                    reprobe = true;  // slot1 holds another key: try slot2
+                    again = true;
+                } else if ((e.x & 0x1FFFFFFu) == want) {
                     v = e.y;
                     const uint32_t kind = e.x >> 25;
                     if (avail >= 4 && kind == 1) {
@@ -300,12 +370,16 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                     }
                 }
             }
-            if (again) {
+            if (reprobe) {
+                nk = fk;
+                np = fp | RT_SLOT2;
+            } else if (again) {
                 nk = node | (d << 23);
-                np = fp | 0x80000000u;
+                np = (fp & ~RT_SLOT2) | 0x80000000u;
+                if (!(fp >> 31)) cnt -= (uint32_t)(ph0 != 0u);  // the placeholder leaves the count
             } else {
-                cnt += (uint32_t)(v != 0u) - ((fp >> 30) & 1u);
-                if (DENSE && v != ph0) out[i - pos0] = v;
+                cnt += (uint32_t)(v != 0u) - ((fp >> 31) ? 0u : (uint32_t)(ph0 != 0u));
+                if (OUTW && V != 6 && v != ph0) put_id<OUTW>(out, i - pos0, v);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -318,37 +392,74 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         __builtin_amdgcn_wave_barrier();
         qn += (uint32_t)__popcll(m);
         r.n = 0;
+        r.keep = 0;
     };
-    auto window = [&](int64_t c, int s) __attribute__((always_inline)) -> const u32x2* {
-        const uint8_t* base = c < c_hi ? text + pos0 + c * RT_CHUNK - 4 : dummy - 4;
-        return reinterpret_cast<const u32x2*>(base + 256 * s + 4 * lane);
+    // Text of chunk c: each lane loads its own aligned dword per group (256
+    // B per instruction, two cache lines), plus one dword before the chunk
+    // that all lanes load (one line); the three look-back bytes of a lane
+    // come from its neighbour by DPP (chunk()).
+    auto fetch = [&](uint32_t (&xr)[4], uint32_t& xp, int64_t c) __attribute__((always_inline)) {
+        const uint8_t* base = c < c_hi ? text + pos0 + c * RT_CHUNK : dummy;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            xr[s] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(base + 256 * s + 4 * lane));
+        xp = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(base - 4));
     };
     auto stand_in_store = [&]() __attribute__((always_inline)) {
-        if (DENSE) {
-            uint4* o = reinterpret_cast<uint4*>(t.scratch);
+        if (OUTW == 4) {
+            u32x4* o = reinterpret_cast<u32x4*>(t.scratch);
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-                __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(o + 64 * s + lane));
+            for (int s = 0; s < 4; ++s) __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, o + 64 * s + lane);
+        }
+        if (OUTW == 2) {
+            u32x2* o = reinterpret_cast<u32x2*>(t.scratch);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) __builtin_nontemporal_store(u32x2{0u, 0u}, o + 64 * s + lane);
         }
     };
     Round rr;
     rr.n = 0;
-    u32x2 xa[4], xb[4];
+    rr.keep = 0;
+    uint32_t xa[4], xb[4], pa, pb;
     int64_t ch = c_lo + (int64_t)blockIdx.x * RT_WAVES + wid;
     // One chunk: depth<=2 answers from LDS, filter, the previous chunk's
     // round consumed and a new one issued, the store,
     // the push of this chunk's candidates, the prefetch two chunks ahead.
-    auto chunk = [&](u32x2 (&x)[4], int64_t c) __attribute__((always_inline)) {
+    auto chunk = [&](uint32_t (&xr)[4], uint32_t& xp, int64_t c) __attribute__((always_inline)) {
         const int64_t pc = pos0 + c * RT_CHUNK;
         if (V == 9) { tB = stamp(); ph[6] += 1; }
+        // 8-byte windows {previous dword, own dword}: wave_shr:1 hands each
+        // lane its left neighbour's dword; lane 0 keeps `old`: the previous
+        // group's lane-63 dword (wave_ror:1 of that group), or for group 0
+        // the dword before the chunk
+        u32x2 x[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t fix = s == 0 ? xp : __builtin_amdgcn_update_dpp(0u, xr[s - 1], 0x13C, 0xf, 0xf, false);
+            x[s].x = __builtin_amdgcn_update_dpp(fix, xr[s], 0x138, 0xf, 0xf, false);  // wave_shr:1
+            x[s].y = xr[s];
+        }
         // position j = 4s + b of this lane is pc + 256s + 4*lane + b; its key
         // is the LE u24 ending at byte b of x[s].y (bytes i-2, i-1, i)
 #define RT_KEY(j) ((uint32_t)((((uint64_t)x[(j) >> 2].y << 32) | x[(j) >> 2].x) >> (8 * (2 + ((j) & 3)))) & 0xFFFFFFu)
         uint32_t res[16];
         uint32_t cm = 0;  // bit j: position j goes past depth 2
 #pragma unroll
-        for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
-        if (V == 0 || V == 9) {
+        for (int j = 0; j < 16; ++j) res[j] = (V >= 2 && V <= 4) ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
+        if (V == 3) {  // streaming + latency-like delay (the wave yields its SIMD)
+#pragma unroll 1
+            for (int k = 0; k < 40; ++k) __builtin_amdgcn_s_sleep(2);
+        }
+        if (V == 4) {  // streaming + ~500 dependent VALU per chunk
+            uint32_t z = res[0];
+#pragma unroll 1
+            for (int k = 0; k < 125; ++k) {
+                z = z * 3u + 1u;
+                z ^= z >> 7;
+            }
+            res[0] ^= (z == 0x12345u);
+        }
+        if (V == 0 || V >= 5) {
             uint32_t fw[16];
 #pragma unroll
             for (int j = 0; j < 16; ++j) fw[j] = s_f[rt_fhash(RT_KEY(j)) >> 20];
@@ -364,24 +475,41 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         }
         cnt += __popc(nzm);
         if (V == 9) { const uint64_t u = stamp(); ph[0] += u - tB; tB = u; }
-        if (V == 0 || V == 9) {
+        if (V == 0 || V >= 5) {
             if (rr.n) consume(rr);                      // the round issued last chunk
             if (V == 9) { const uint64_t u = stamp(); ph[3] += u - tB; tB = u; }
-            issue(rr, qn >= RT_ROUND ? RT_ROUND : 0u);  // items of earlier chunks (stores issued)
+            issue(rr, qn >= RT_ROUND ? qn : 0u);  // items of earlier chunks (stores issued)
             if (V == 9) { const uint64_t u = stamp(); ph[5] += u - tB; tB = u; }
         }
         // store the chunk: depth<=2 answers, queued positions patched later
-        if (DENSE) {
-            uint4* o = reinterpret_cast<uint4*>(out + (pc - pos0));
+        if (OUTW == 4 && V != 10) {
+            u32x4* o = reinterpret_cast<u32x4*>(reinterpret_cast<uint32_t*>(out) + (pc - pos0));
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 u32x4 v = {res[4 * s], res[4 * s + 1], res[4 * s + 2], res[4 * s + 3]};
-                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o + 64 * s + lane));
+                __builtin_nontemporal_store(v, o + 64 * s + lane);
+            }
+        }
+        if (OUTW == 4 && V == 10) {  // ablation: sc1 (L2-dropping) chunk stores
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<uint32_t*>(out) + (pc - pos0), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                u32x4 v = {res[4 * s], res[4 * s + 1], res[4 * s + 2], res[4 * s + 3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs, (1024 * s + 16 * lane), 0, 16);
+            }
+        }
+        if (OUTW == 2) {  // 512 contiguous bytes per store instruction
+            u32x2* o = reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(out) + (pc - pos0));
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                u32x2 v = {res[4 * s] | (res[4 * s + 1] << 16), res[4 * s + 2] | (res[4 * s + 3] << 16)};
+                __builtin_nontemporal_store(v, o + 64 * s + lane);
             }
         }
         asm volatile("" ::: "memory");  // the store stays ahead of any later probe
         if (V == 9) { const uint64_t u = stamp(); ph[4] += u - tB; tB = u; }
-        if (V == 0 || V == 9) {
+        if (V == 0 || V >= 5) {
             // lane count c = popc(cm); exclusive wave prefix by a DPP scan;
             // items written by a loop over the lane's own set bits
             const uint32_t c = __popc(cm);
@@ -389,8 +517,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             const uint32_t base = incl - c;
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
             for (uint32_t done = 0;;) {  // wave-uniform
-                // room for the in-flight rounds' survivors is kept
-                const uint32_t room = RT_QCAP - qn - rr.n;
+                // the in-flight round's possible survivors keep their room
+                const uint32_t room = RT_QCAP - qn - rr.keep;
                 uint32_t mm = cm, rank = base;
                 while (mm) {  // per lane: its own candidates, in position order
                     const uint32_t j = __builtin_ctz(mm);
@@ -404,7 +532,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                         // text[i-3..i] = window bytes 1+b .. 4+b (alignbit uses
                         // the shift mod 32, so b = 3 is the high word itself)
                         qkey[slot] = b == 3 ? w.y : __builtin_amdgcn_alignbit(w.y, w.x, 8 * (1 + b));
-                        qpos[slot] = ((uint32_t)(pc - pos0) + 256 * sg + 4 * lane + b) | (((nzm >> j) & 1u) << 30);
+                        qpos[slot] = (uint32_t)(pc - pos0) + 256 * sg + 4 * lane + b;
                     }
                     ++rank;
                 }
@@ -412,45 +540,42 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 qn += took;
                 done += took;
                 if (done == total) break;
-                // queue full (dense matches): resolve synchronously in
+                // ring full (dense matches): resolve synchronously in
                 // separate registers; these waits cover this chunk's stores
                 if (rr.n) {
                     consume(rr);
                 } else {
                     Round rs;
-                    issue(rs, qn < RT_ROUND ? qn : RT_ROUND);
+                    issue(rs, qn);
                     consume(rs);
                 }
             }
             if (V == 9) { const uint64_t u = stamp(); ph[1] += u - tB; tB = u; }
         }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) x[s] = __builtin_nontemporal_load(window(c + 2 * stride, s));
+        fetch(xr, xp, c + 2 * stride);
     };
     // Enter the loop with the memory-op pattern of the steady state (round,
     // store, prefetch; round, store, prefetch) so the compiler's vmcnt is the
     // steady-state one.
     Round r0;
-    if (V == 0 || V == 9) issue(r0, 0);
+    if (V == 0 || V >= 5) issue(r0, 0);
     stand_in_store();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) xa[s] = __builtin_nontemporal_load(window(ch, s));
-    if (V == 0 || V == 9) issue(rr, 0);
+    fetch(xa, pa, ch);
+    if (V == 0 || V >= 5) issue(rr, 0);
     stand_in_store();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) xb[s] = __builtin_nontemporal_load(window(ch + stride, s));
+    fetch(xb, pb, ch + stride);
     for (;;) {  // wave-uniform
         if (ch >= c_hi) break;
-        chunk(xa, ch);
+        chunk(xa, pa, ch);
         if (ch + stride >= c_hi) break;
-        chunk(xb, ch + stride);
+        chunk(xb, pb, ch + stride);
         ch += 2 * stride;
     }
-    if (V == 0 || V == 9) {
+    if (V == 0 || V >= 5) {
         if (rr.n) consume(rr);
         while (qn) {  // wave-uniform; every round advances each item
             Round rs;
-            issue(rs, qn < RT_ROUND ? qn : RT_ROUND);
+            issue(rs, qn);
             consume(rs);
         }
     }
@@ -475,7 +600,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 for (int b = 0; b < 4; ++b) {
                     if (p + b < pos0 + n) {
                         const uint32_t v = rt_one(text, s_t, t, p + b, stream_start);
-                        if (DENSE) out[p + b - pos0] = v;
+                        if (OUTW) put_id<OUTW>(out, p + b - pos0, v);
                         cnt += v != 0u;
                     }
                 }
@@ -490,8 +615,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
 
 constexpr int DFA_THREADS = 256;
 
+template <int OUTW>
 __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
-                                                               int64_t pos0, int64_t n, uint32_t* __restrict__ out,
+                                                               int64_t pos0, int64_t n, void* __restrict__ out,
                                                                unsigned long long* __restrict__ count, DfaDev t,
                                                                int64_t seg_len) {
     const int64_t nseg = (n + seg_len - 1) / seg_len;
@@ -514,12 +640,17 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
                 s = t.next[(size_t)s * 256 + ((W[j >> 2] >> (8 * (j & 3))) & 0xFFu)];
                 r[j] = t.out[s];
             }
-            if (out) {
-                uint4* o = reinterpret_cast<uint4*>(out + (i - pos0));
+            if (OUTW == 4) {
+                uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
                 o[0] = make_uint4(r[0], r[1], r[2], r[3]);
                 o[1] = make_uint4(r[4], r[5], r[6], r[7]);
                 o[2] = make_uint4(r[8], r[9], r[10], r[11]);
                 o[3] = make_uint4(r[12], r[13], r[14], r[15]);
+            }
+            if (OUTW == 2) {
+                uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + (i - pos0));
+                o[0] = make_uint4(r[0] | r[1] << 16, r[2] | r[3] << 16, r[4] | r[5] << 16, r[6] | r[7] << 16);
+                o[1] = make_uint4(r[8] | r[9] << 16, r[10] | r[11] << 16, r[12] | r[13] << 16, r[14] | r[15] << 16);
             }
 #pragma unroll
             for (int j = 0; j < 16; ++j) cnt += r[j] != 0u;
@@ -527,7 +658,7 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
         for (; i < hi; ++i) {
             s = t.next[(size_t)s * 256 + text[i]];
             const uint32_t v = t.out[s];
-            if (out) out[i - pos0] = v;
+            if (OUTW) put_id<OUTW>(out, i - pos0, v);
             cnt += v != 0u;
         }
     }
@@ -546,16 +677,19 @@ __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint6
 }  // namespace
 
 static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
-                                 uint32_t* out, unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s,
-                                 int blocks_override) {
+                                 void* out, int outw, unsigned long long* count, const RtDev& t, int num_cu,
+                                 hipStream_t s, int blocks_override) {
     if (n <= 0) return hipSuccess;
+    if (!out) outw = 0;
+    if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // queued positions are kept as 30-bit offsets from pos0: split huge scans
-    constexpr int64_t PIECE = (int64_t)1 << 30;
+    constexpr int64_t PIECE = (int64_t)RT_POSMASK + 1;
     if (n > PIECE) {
         for (int64_t off = 0; off < n; off += PIECE) {
             const int64_t m = n - off < PIECE ? n - off : PIECE;
-            hipError_t e = launch_rt_impl(variant, text, stream_start, pos0 + off, m, out ? out + off : nullptr,
-                                          count, t, num_cu, s, blocks_override);
+            void* o = outw ? reinterpret_cast<uint8_t*>(out) + off * outw : nullptr;
+            hipError_t e = launch_rt_impl(variant, text, stream_start, pos0 + off, m, o, outw, count, t, num_cu, s,
+                                          blocks_override);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
@@ -565,16 +699,23 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
     if (blocks > num_cu) blocks = num_cu;  // persistent: one 1024-lane workgroup per CU (LDS-bound)
     if (blocks_override > 0) blocks = blocks_override;
     const dim3 g((unsigned)blocks), b(RT_THREADS);
-#define RT_LAUNCH(VV)                                                                                        \
-    do {                                                                                                     \
-        if (out)                                                                                             \
-            hipLaunchKernelGGL((rt_scan_kernel<VV, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
-        else                                                                                                 \
-            hipLaunchKernelGGL((rt_scan_kernel<VV, false>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
+#define RT_LAUNCH(VV)                                                                                             \
+    do {                                                                                                          \
+        if (outw == 4)                                                                                            \
+            hipLaunchKernelGGL((rt_scan_kernel<VV, 4>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
+        else if (outw == 2)                                                                                       \
+            hipLaunchKernelGGL((rt_scan_kernel<VV, 2>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
+        else                                                                                                      \
+            hipLaunchKernelGGL((rt_scan_kernel<VV, 0>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
     } while (0)
     switch (variant) {
         case 1: RT_LAUNCH(1); break;
         case 2: RT_LAUNCH(2); break;
+        case 3: RT_LAUNCH(3); break;
+        case 4: RT_LAUNCH(4); break;
+        case 5: RT_LAUNCH(5); break;
+        case 6: RT_LAUNCH(6); break;
+        case 10: RT_LAUNCH(10); break;
         case 9: RT_LAUNCH(9); break;
         default: RT_LAUNCH(0);
     }
@@ -582,20 +723,22 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
     return hipGetLastError();
 }
 
-hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
+hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                         unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s) {
-    return launch_rt_impl(0, text, stream_start, pos0, n, out, count, t, num_cu, s, 0);
+    return launch_rt_impl(0, text, stream_start, pos0, n, out, outw, count, t, num_cu, s, 0);
 }
 
 hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
-                                uint32_t* out, unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s,
-                                int blocks_override) {
-    return launch_rt_impl(variant, text, stream_start, pos0, n, out, count, t, num_cu, s, blocks_override);
+                                void* out, int outw, unsigned long long* count, const RtDev& t, int num_cu,
+                                hipStream_t s, int blocks_override) {
+    return launch_rt_impl(variant, text, stream_start, pos0, n, out, outw, count, t, num_cu, s, blocks_override);
 }
 
-hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
+hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s) {
     if (n <= 0) return hipSuccess;
+    if (!out) outw = 0;
+    if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // enough segments for ~8 waves per CU, each at least 2 KiB so the
     // max_len-1 warm-up stays a small fraction
     const int64_t lanes = (int64_t)num_cu * 512;
@@ -605,8 +748,13 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     const int64_t nseg = (n + seg - 1) / seg;
     int64_t blocks = (nseg + DFA_THREADS - 1) / DFA_THREADS;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(dfa_scan_kernel, dim3((unsigned)blocks), dim3(DFA_THREADS), 0, s, text, stream_start, pos0, n,
-                       out, count, t, seg);
+    const dim3 g((unsigned)blocks), b(DFA_THREADS);
+    if (outw == 4)
+        hipLaunchKernelGGL(dfa_scan_kernel<4>, g, b, 0, s, text, stream_start, pos0, n, out, count, t, seg);
+    else if (outw == 2)
+        hipLaunchKernelGGL(dfa_scan_kernel<2>, g, b, 0, s, text, stream_start, pos0, n, out, count, t, seg);
+    else
+        hipLaunchKernelGGL(dfa_scan_kernel<0>, g, b, 0, s, text, stream_start, pos0, n, out, count, t, seg);
     return hipGetLastError();
 }
 

@@ -117,10 +117,10 @@ void ensure_stage(PmHip* o, size_t positions) {
     o->stage_cap = cap;
 }
 
-hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* out,
+hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                   unsigned long long* count, hipStream_t s) {
-    if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, count, o->rt, o->num_cu, s);
-    return pm_launch_dfa(text, stream_start, pos0, n, out, count, o->dfa, o->num_cu, s);
+    if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, o->rt, o->num_cu, s);
+    return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
 }
 
 // Scan n new bytes after the carried history; gids to out_gid.
@@ -142,7 +142,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid) {
         std::memset(o->h_stage + ctx + m, 0, 16);
         PM_CHECK(hipMemcpyAsync(o->d_stage, o->h_stage, ctx + m + 16, hipMemcpyHostToDevice, o->stream));
         PM_CHECK(hipEventRecord(o->ev0, o->stream));
-        PM_CHECK(launch(o, o->d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, o->d_res, nullptr, o->stream));
+        PM_CHECK(launch(o, o->d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, o->d_res, 4, nullptr, o->stream));
         PM_CHECK(hipEventRecord(o->ev1, o->stream));
         PM_CHECK(hipMemcpyAsync(o->h_res, o->d_res, m * sizeof(uint32_t), hipMemcpyDeviceToHost, o->stream));
         PM_CHECK(hipStreamSynchronize(o->stream));
@@ -295,8 +295,8 @@ static void fill_slot(PmMpsElem* slot, const char* name, void* (*create_fn)(void
 void pm_mps_hip_rt_register(PmMpsElem* slot) { fill_slot(slot, "HIP Reverse-Trie", pm_hip_rt_create); }
 void pm_mps_hip_ac_register(PmMpsElem* slot) { fill_slot(slot, "HIP Aho-Corasick DFA", pm_hip_ac_create); }
 
-int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0, int64_t n,
-                       uint32_t* d_out, unsigned long long* d_count, void* hip_stream) {
+static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0, int64_t n, void* d_out,
+                       int outw, unsigned long long* d_count, void* hip_stream) {
     PmHip* o = as(obj);
     if (!o->compiled) { std::snprintf(g_err, sizeof(g_err), "not compiled"); return -1; }
     if (pos0 % 16 || stream_start > pos0 || stream_start < 0 || n < 0 || ((uintptr_t)d_text & 15) ||
@@ -304,8 +304,13 @@ int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
         std::snprintf(g_err, sizeof(g_err), "bad arguments (pos0 %% 16, stream_start <= pos0, 16-B alignment)");
         return -2;
     }
+    if (outw == 2 && d_out && o->gids.index_of_gid.size() > 65536) {
+        std::snprintf(g_err, sizeof(g_err), "u16 ids need fewer than 65536 patterns (have %zu)",
+                      o->gids.index_of_gid.size() - 1);
+        return -4;
+    }
     hipError_t e = hipSetDevice(o->device);
-    if (e == hipSuccess) e = launch(o, d_text, stream_start, pos0, n, d_out, d_count, (hipStream_t)hip_stream);
+    if (e == hipSuccess) e = launch(o, d_text, stream_start, pos0, n, d_out, outw, d_count, (hipStream_t)hip_stream);
     if (e != hipSuccess) {
         std::snprintf(g_err, sizeof(g_err), "launch: %s", hipGetErrorString(e));
         return -3;
@@ -313,12 +318,22 @@ int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
     return 0;
 }
 
+int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0, int64_t n,
+                       uint32_t* d_out, unsigned long long* d_count, void* hip_stream) {
+    return scan_device(obj, d_text, stream_start, pos0, n, d_out, 4, d_count, hip_stream);
+}
+
+int pm_hip_scan_device16(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0, int64_t n,
+                         uint16_t* d_out, unsigned long long* d_count, void* hip_stream) {
+    return scan_device(obj, d_text, stream_start, pos0, n, d_out, 2, d_count, hip_stream);
+}
+
 // Timing-only ablation launches of the RT kernel (bench_variants.py).
-int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, uint32_t* d_out,
+int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out, int out_width,
                               unsigned long long* d_count, void* hip_stream, int blocks) {
     PmHip* o = as(obj);
     if (o->kind != KIND_RT) return -1;
-    hipError_t e = pm_launch_rt_variant(variant, d_text, 0, 0, n, d_out, d_count, o->rt, o->num_cu,
+    hipError_t e = pm_launch_rt_variant(variant, d_text, 0, 0, n, d_out, out_width, d_count, o->rt, o->num_cu,
                                         (hipStream_t)hip_stream, blocks);
     return e == hipSuccess ? 0 : -3;
 }

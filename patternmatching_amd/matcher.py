@@ -169,9 +169,11 @@ class HipMatcher:
         """(file << 24 | line) per position, the golden-fixture format."""
         return self._codes[self.read_block_gids(data)]
 
-    def scan_device(self, d_text_ptr, stream_start, pos0, n, d_out_ptr, d_count_ptr, stream_ptr):
-        rc = self.lib.pm_hip_scan_device(self.obj, d_text_ptr, stream_start, pos0, n, d_out_ptr, d_count_ptr,
-                                         stream_ptr)
+    def scan_device(self, d_text_ptr, stream_start, pos0, n, d_out_ptr, d_count_ptr, stream_ptr, out_width=4):
+        """Device-resident scan (pm_hip_scan_device / _scan_device16): ids of
+        out_width bytes (4 = u32, 2 = u16) to d_out_ptr, or count only."""
+        fn = {4: self.lib.pm_hip_scan_device, 2: self.lib.pm_hip_scan_device16}[out_width]
+        rc = fn(self.obj, d_text_ptr, stream_start, pos0, n, d_out_ptr, d_count_ptr, stream_ptr)
         if rc != 0:
             raise RuntimeError(self.lib.pm_hip_last_error().decode())
 

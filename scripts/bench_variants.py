@@ -19,9 +19,10 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--stream", type=int, default=0)
 ap.add_argument("--variants", default="0,1,2")
 ap.add_argument("--blocks", default="0")
-ap.add_argument("--modes", default="dense,count")
+ap.add_argument("--modes", default="dense,dense16,count")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
+WIDTH = {"dense": 4, "dense16": 2, "count": 0}
 data = os.path.join(REPO, "tests", "golden", "data")
 lib = pm.load()
 d = pm.Dictionary([os.path.join(data, x) for x in DICTS[args.dict]])
@@ -41,8 +42,8 @@ for r in range(args.rounds + 1):
     for (v, mode, b) in variants:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        rc = lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, out.data_ptr() if mode == "dense" else None,
-                                           cnt.data_ptr(), s.cuda_stream, b)
+        rc = lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, out.data_ptr() if mode != "count" else None,
+                                           WIDTH[mode], cnt.data_ptr(), s.cuda_stream, b)
         assert rc == 0
         e1.record(s)
         torch.cuda.synchronize()
@@ -50,24 +51,24 @@ for r in range(args.rounds + 1):
             times[(v, mode, b)].append(e0.elapsed_time(e1))
 res = {}
 if "9" in args.variants.split(","):
-    for mode in ("dense", "count"):
+    for mode in args.modes.split(","):
         cnt.zero_()
-        lib.pm_hip_debug_scan_variant(m.obj, 9, text.data_ptr(), n, out.data_ptr() if mode == "dense" else None,
-                                      cnt.data_ptr(), s.cuda_stream, 0)
+        lib.pm_hip_debug_scan_variant(m.obj, 9, text.data_ptr(), n, out.data_ptr() if mode != "count" else None,
+                                      WIDTH[mode], cnt.data_ptr(), s.cuda_stream, 0)
         torch.cuda.synchronize()
         c = [int(x) for x in cnt.tolist()]
         names = ["lds_filter", "push", "round_wait", "consume", "store", "issue", "chunks", "total"]
         res[f"v9-stamps-{mode}"] = {k: (c[i] / c[6] if i != 6 else c[i]) for i, k in enumerate(names)}
-for v in (7, 8):
+for v in ():
     if str(v) in args.variants.split(","):
         cnt.zero_()
-        lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, None, cnt.data_ptr(), s.cuda_stream, 0)
+        lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, None, 0, cnt.data_ptr(), s.cuda_stream, 0)
         torch.cuda.synchronize()
         res[f"v{v}-counter"] = {"value": int(cnt.item()), "per_position": int(cnt.item()) / n}
 for (v, mode, b), t in times.items():
-    if v in (7, 8, 9):
+    if v == 9:
         continue
     ms = statistics.median(t)
     res[f"v{v}-{mode}-b{b}"] = {"ms": round(ms, 4), "min": round(min(t), 4), "GBps_stream": round(n / ms / 1e6, 1),
-                                "alg_GBps": round(n * (5 if mode == "dense" else 1) / ms / 1e6, 1)}
+                                "alg_GBps": round(n * (1 + WIDTH[mode]) / ms / 1e6, 1)}
 print(json.dumps(res, indent=1))

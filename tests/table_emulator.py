@@ -49,9 +49,30 @@ def filter_maybe(filt, key24):
     f = (np.asarray(key24).astype(np.uint64) * np.uint64(0x9E3779)) & np.uint64(0xFFFFFFFF)
     w = filt[(f >> np.uint64(20)).astype(np.int64)].astype(np.uint64)
     m = np.zeros_like(f)
-    for sh in (5, 10, 15):
+    for sh in (0, 8, 16):
         m |= np.uint64(1) << ((f >> np.uint64(sh)) & np.uint64(31))
     return (w & m) == m
+
+
+def _bits(w, g):
+    ok = np.ones(len(g), bool)
+    for sh in (0, 8, 16):
+        ok &= ((w >> ((g >> np.uint64(sh)) & np.uint64(31))) & np.uint64(1)) == 1
+    return ok
+
+
+def filter2_maybe(filt, key24, c3):
+    """Stage 2 (pm_rt_p3hash / pm_rt_s4hash): a 3-byte pattern, or a depth-4
+    suffix text[i-3..i]."""
+    M = np.uint64(0xFFFFFFFF)
+    f2 = filt[FILTER_WORDS:].astype(np.uint64)
+    k = np.asarray(key24).astype(np.uint64)
+    g3 = (k * np.uint64(0x85EBCA)) & M
+    hit3 = _bits(f2[(g3 >> np.uint64(24)).astype(np.int64)], g3)
+    k32 = (k << np.uint64(8)) | np.asarray(c3).astype(np.uint64)
+    g4 = (k32 * np.uint64(0x9E3779B1)) & M
+    w4 = f2[(256 + (((g4 >> np.uint64(20)) * np.uint64(7)) >> np.uint64(4))).astype(np.int64)]
+    return hit3 | _bits(w4, g4)
 
 
 def t3h_lookup(t3h, bits, key24):
@@ -99,7 +120,8 @@ def rt_scan(img, text, stream_start=0, use_filter=True):
     key24 = c2 | (c1 << 8) | (c0 << 16)
     cont = ((v & 0x8000) != 0) & (avail >= 3)
     if use_filter:
-        cont &= filter_maybe(filt, key24)
+        c3 = np.concatenate([[0, 0, 0], text[:-3]]).astype(np.uint32)
+        cont &= filter_maybe(filt, key24) & filter2_maybe(filt, key24, c3)
     for p in i[cont]:
         e = t3h_lookup(t3h, bits, int(key24[p]))
         if e is None:

@@ -247,6 +247,58 @@ def test_count_only_mode(kind):
     assert np.array_equal(m._codes[out.cpu().numpy().view(np.uint32)], exp)
 
 
+@pytest.mark.parametrize("kind", KINDS)
+def test_u16_ids_equal_u32_ids(kind):
+    """pm_hip_scan_device16: the compact id stream is the u32 one, narrowed,
+    on random text and on the adversarial tiling (deep walks, dense queue),
+    including unaligned tails and context-only heads."""
+    torch = _torch()
+    s = torch.cuda.current_stream().cuda_stream
+    m = matcher("merged", kind)
+    rnd = pm.gen_stream(3_000_017, 9, 0)
+    adv = np.tile(SHIP, 30)
+    for text in (rnd, adv):
+        n = len(text)
+        dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+        for pos0, ss in ((0, 0), (4096, 4096 - (m.max_pattern_len - 1)), (4096, 4096)):
+            ss = max(ss, 0)
+            w = n - pos0
+            a = torch.zeros(w, dtype=torch.int32, device="cuda")
+            b = torch.full((w + 8,), 0x7777, dtype=torch.int16, device="cuda")
+            ca = torch.zeros(1, dtype=torch.int64, device="cuda")
+            cb = torch.zeros(1, dtype=torch.int64, device="cuda")
+            m.scan_device(dt.data_ptr(), ss, pos0, w, a.data_ptr(), ca.data_ptr(), s)
+            m.scan_device(dt.data_ptr(), ss, pos0, w, b.data_ptr(), cb.data_ptr(), s, out_width=2)
+            torch.cuda.synchronize()
+            a32 = a.cpu().numpy().view(np.uint32)
+            b16 = b.cpu().numpy().view(np.uint16)
+            assert a32.max() < 65536
+            assert np.array_equal(b16[:w].astype(np.uint32), a32), (n, pos0, ss)
+            assert np.all(b16[w:] == 0x7777)  # nothing written past n
+            assert int(ca.item()) == int(cb.item()) == int(np.count_nonzero(a32))
+    o = oracle_for("merged")
+    o.reset()
+    exp = o.scan_codes(rnd[:1 << 20])
+    b = torch.zeros(1 << 20, dtype=torch.int16, device="cuda")
+    dt = torch.from_numpy(np.concatenate([rnd, np.zeros(64, np.uint8)])).cuda()
+    m.scan_device(dt.data_ptr(), 0, 0, 1 << 20, b.data_ptr(), None, s, out_width=2)
+    torch.cuda.synchronize()
+    assert np.array_equal(m._codes[b.cpu().numpy().view(np.uint16).astype(np.uint32)], exp)
+
+
+def test_u16_ids_refused_for_large_dictionaries():
+    torch = _torch()
+    pats = [b"%05dxq" % k for k in range(70000)]
+    m = pm.HipMatcher("rt")
+    m.add_dictionary(pm.Dictionary(patterns=pats))
+    m.compile()
+    dt = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    b = torch.zeros(4096, dtype=torch.int16, device="cuda")
+    with pytest.raises(RuntimeError, match="65536"):
+        m.scan_device(dt.data_ptr(), 0, 0, 4096, b.data_ptr(), None, torch.cuda.current_stream().cuda_stream,
+                      out_width=2)
+
+
 @pytest.mark.slow
 def test_full_size_snort_1gib_kernels_agree():
     """BASELINE config 3 size (snort, 1 GiB): the two independent kernels agree
@@ -266,6 +318,11 @@ def test_full_size_snort_1gib_kernels_agree():
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert int(ca.item()) == int(cb.item()) == int((a != 0).sum().item())
+    c = torch.empty(n, dtype=torch.int16, device="cuda")  # the bench's compact id stream
+    rt.scan_device(dt.data_ptr(), 0, 0, n, c.data_ptr(), None, s, out_width=2)
+    torch.cuda.synchronize()
+    assert torch.equal(c.to(torch.int32) & 0xFFFF, a)
+    del c
     o = oracle_for("snort")
     W = o.max_len - 1
     rng = np.random.default_rng(0)

@@ -9,7 +9,7 @@ import pytest
 
 import patternmatching_amd as pm
 from oracle_lib import DATA, GOLDEN, dict_paths, oracle_for
-from table_emulator import FlatImage, dfa_scan, gid_to_code, rt_scan
+from table_emulator import FlatImage, dfa_scan, filter2_maybe, filter_maybe, gid_to_code, rt_scan
 
 MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
 SHIP = np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8)
@@ -70,6 +70,35 @@ def test_rt_filter_has_no_false_negatives_and_few_positives(key):
     # performance bound, not correctness: 3 bits/key in 4096 words queue
     # ~1.8% (snort) to ~3% (merged, 16k keys) of random-ASCII positions
     assert passed.mean() < 0.035, passed.mean()
+
+
+@pytest.mark.parametrize("key", ["et", "snort", "merged"])
+def test_rt_stage2_filter_keeps_every_answer_changing_suffix(key):
+    """Stage 2 passes every 3-byte pattern (any text[i-3]) and every 4-byte
+    suffix that is a depth-4 node, so a position it drops has the depth-2
+    answer; and it drops most stage-1 candidates of random text."""
+    d, img, _ = image(key, pm.KIND_RT)
+    filt = img.array("filt")
+    pats = d.patterns()
+    p3 = np.array(sorted({p[2] | p[1] << 8 | p[0] << 16 for p in (q[::-1] for q in pats if len(q) == 3)}),
+                  np.uint32)
+    s4 = sorted({(p[2] | p[1] << 8 | p[0] << 16, p[3]) for p in (q[::-1] for q in pats if len(q) >= 4)})
+    assert len(p3) > 100 and len(s4) > 5000
+    for c3 in (0, 0x41, 0xFF):
+        assert filter2_maybe(filt, p3, np.full(len(p3), c3, np.uint32)).all()
+    s4k = np.array([a for a, _ in s4], np.uint32)
+    s4c = np.array([b for _, b in s4], np.uint32)
+    assert filter2_maybe(filt, s4k, s4c).all()
+    text = pm.gen_stream(1 << 18, seed=13, mode=0)
+    t = text.astype(np.uint32)
+    key24 = t[1:-2] | (t[2:-1] << 8) | (t[3:] << 16)
+    t12 = img.array("t12").astype(np.uint32)
+    stage1 = ((t12[key24 >> 8] & 0x8000) != 0) & filter_maybe(filt, key24)
+    stage2 = stage1 & filter2_maybe(filt, key24, t[:-3])
+    assert stage1.sum() > 1000
+    # performance bound, not correctness: stage 2 keeps ~30 % (snort) to
+    # ~45 % (merged) of the stage-1 candidates of random ASCII
+    assert stage2.sum() < 0.55 * stage1.sum(), (stage2.sum(), stage1.sum())
 
 
 def test_rt_image_context():
