@@ -105,7 +105,10 @@ def main():
     import patternmatching_amd as pm
 
     torch.cuda.set_device(local)
-    if world > 1:
+    # the RCCL path runs for world > 1; PM_BENCH_DIST=1 runs it at world 1 too
+    # (one-GPU rehearsal of the multi-GPU code: init, barriers, all-reduces)
+    use_dist = world > 1 or os.environ.get("PM_BENCH_DIST") == "1"
+    if use_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     lib = pm.load()
     lib.pm_hip_set_device(local)
@@ -133,7 +136,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     count.zero_()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -145,14 +148,14 @@ def main():
         evs[k][1].record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = t1 - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
 
     stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
     matches = count.clone()
-    if world > 1:
+    if use_dist:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(matches, op=dist.ReduceOp.SUM)  # RCCL over xGMI: the match-count reduction
     elapsed, kernel_ms = stats.tolist()
@@ -206,7 +209,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
