@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-sample", type=int, default=256 << 20, help="bytes of the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--score", action="store_true",
+                   help="after timing, score the ids against the AC-DFA reliable instance on the device "
+                        "(measure.c:174-190) and report FP/FN/partial rates (dense mode)")
     return p.parse_args()
 
 
@@ -158,6 +161,34 @@ def main():
     if use_dist:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(matches, op=dist.ReduceOp.SUM)  # RCCL over xGMI: the match-count reduction
+    # after the timed region: all-matches (patterns ending at each position,
+    # i.e. the suffix-chain length of each id) and, with --score, accuracy
+    # against the reliable AC instance, both by pm_hip_score_device
+    extra = {}
+    if width == 4:
+        sc = torch.zeros(5, dtype=torch.int64, device="cuda")
+        m.score_device(out.data_ptr(), out.data_ptr(), n, sc.data_ptr(), stream.cuda_stream)
+        allm = sc.clone()
+        if args.score:
+            ac = pm.HipMatcher("ac")
+            ac.add_dictionary(d)
+            ac.compile()
+            ref = torch.empty(n, dtype=torch.int32, device="cuda")
+            ac.scan_device(text.data_ptr(), 0, 0, n, ref.data_ptr(), None, stream.cuda_stream)
+            sc.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            m.score_device(out.data_ptr(), ref.data_ptr(), n, sc.data_ptr(), stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            c = [int(v) for v in sc.tolist()]
+            extra["accuracy"] = {"reliable": "AC dense DFA (HIP)", "positions": n, "success": c[0],
+                                 "false_pos_rate": c[3] / n, "false_neg_rate": c[2] / n, "partial_rate": c[1] / n,
+                                 "score_ms": round(e0.elapsed_time(e1), 4)}
+            del ref
+        if use_dist:
+            dist.all_reduce(allm, op=dist.ReduceOp.SUM)
+        extra["all_matches_per_step"] = int(allm[4].item())
     elapsed, kernel_ms = stats.tolist()
     total_matches = int(matches.item())
 
@@ -195,6 +226,9 @@ def main():
             },
             "matches_per_sec": round(total_matches / elapsed, 1),
             "matches_per_step": total_matches // max(1, args.steps),
+            **({"all_matches_per_sec": round(extra["all_matches_per_step"] * args.steps / elapsed, 1)}
+               if "all_matches_per_step" in extra else {}),
+            **extra,
             "kernel_ms": round(kernel_ms, 4),
             "roofline": {
                 "bound": "hbm",

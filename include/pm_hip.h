@@ -85,6 +85,22 @@ int pm_hip_scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
 int pm_hip_scan_device16(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0,
                          int64_t n, uint16_t* d_out, unsigned long long* d_count, void* hip_stream);
 
+/* Accuracy of one dense u32 gid stream against a reference one, on the
+ * device (the scoring of Core/src/measure.c:174-190 with is_pattern_suffix,
+ * PatternsTree.c:485-494): per position, equal -> success; d_algo's pattern
+ * a proper suffix (ancestor) of d_real's -> partial; d_algo none -> false
+ * negative; else false positive.  Also all-matches: the number of patterns
+ * ending at each position of d_real (its suffix chain), summed.  Both
+ * arrays come from objects compiled from the same patterns in the same add
+ * order (RT and AC objects then share gids).  d_counts (5 device u64) +=
+ * {success, partial, false_neg, false_pos, all_matches}.  16-B aligned.
+ * Asynchronous. */
+int pm_hip_score_device(void* obj, const uint32_t* d_algo, const uint32_t* d_real, int64_t n,
+                        unsigned long long* d_counts, void* hip_stream);
+/* The patterns-tree parent of a gid (longest proper suffix pattern, 0 = none);
+ * UINT32_MAX when out of range. */
+uint32_t pm_hip_parent_gid(void* obj, uint32_t gid);
+
 /* Device-side synthetic stream, identical to pm_gen_stream_host(). */
 int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
                              void* hip_stream);

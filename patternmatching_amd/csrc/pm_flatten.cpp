@@ -236,6 +236,25 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
     return im;
 }
 
+PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap& g) {
+    // In the trie of the reversed patterns the nodes above a pattern's node
+    // are its suffixes, so its parent is the deepest pattern strictly above.
+    BfsTrie t = build_trie(pats, g, /*reversed=*/true);
+    std::vector<uint32_t> best(t.n, 0);
+    PmParents r;
+    r.parent.assign(g.index_of_gid.size(), 0);
+    r.depth.assign(g.index_of_gid.size(), 0);
+    for (uint32_t v = 1; v < t.n; ++v) {  // BFS order: parents first
+        const uint32_t up = best[t.parent[v]];
+        if (t.gid[v]) {
+            r.parent[t.gid[v]] = up;
+            r.depth[t.gid[v]] = 1 + (up ? r.depth[up] : 0);
+        }
+        best[v] = t.gid[v] ? t.gid[v] : up;
+    }
+    return r;
+}
+
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
     DfaImage im;
     BfsTrie t = build_trie(pats, g, /*reversed=*/false);

@@ -78,11 +78,21 @@ struct DfaImage {
     size_t bytes() const { return next.size() * 4 + out.size() * 4; }
 };
 
+// Pattern suffix relation in gid space (the reference's patterns tree,
+// PatternsTree.c:180-217 / 388-397: a pattern's parent is its longest proper
+// suffix that is a pattern): parent[g] (0 = none) and depth[g] = the number
+// of patterns on g's parent chain including g = how many patterns end at a
+// position whose answer is g.  parent[0] = depth[0] = 0.
+struct PmParents {
+    std::vector<uint32_t> parent, depth;
+};
+
 // Patterns are given in add_pattern order; duplicates are not expected (the
 // host front end de-duplicates) but are tolerated: the first one wins.
 PmGidMap pm_assign_gids(const std::vector<std::string>& pats);
 RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g);
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g);
+PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap& g);
 
 constexpr uint32_t RT_T1_BASE = 65536;   // t12[65536 + c]: lookback of exactly one byte
 constexpr uint32_t RT_CONT16 = 0x8000u;  // t12: depth-2 node has children (low 15 bits: best so far)

@@ -668,6 +668,55 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
     }
 }
 
+// Accuracy of one id stream against a reference one (Core/src/measure.c:
+// 174-190 with is_pattern_suffix, PatternsTree.c:485-494), one position per
+// lane-element: equal -> success; algo on real's parent chain -> partial;
+// algo none -> false negative; else false positive.  all_matches adds
+// depth[real] (patterns ending at the position).  counts[0..4] += success,
+// partial, false_neg, false_pos, all_matches.  HBM-bound: 8 B per position.
+__device__ __forceinline__ void score_one(uint32_t a, uint32_t r, const uint32_t* __restrict__ parent,
+                                          const uint32_t* __restrict__ depth, uint32_t (&c)[5]) {
+    if (a == r) {
+        ++c[0];
+    } else if (a) {
+        uint32_t cur = r;
+        while (cur && cur != a) cur = parent[cur];
+        ++c[cur ? 1 : 3];
+    } else {
+        ++c[2];
+    }
+    if (r) c[4] += depth[r];
+}
+
+constexpr int SCORE_THREADS = 256;
+
+__global__ __launch_bounds__(SCORE_THREADS) void score_kernel(const uint32_t* __restrict__ algo,
+                                                              const uint32_t* __restrict__ real, int64_t n,
+                                                              const uint32_t* __restrict__ parent,
+                                                              const uint32_t* __restrict__ depth,
+                                                              unsigned long long* __restrict__ counts) {
+    uint32_t c[5] = {0, 0, 0, 0, 0};
+    const int64_t nv = n / 4;
+    const int64_t stride = (int64_t)gridDim.x * SCORE_THREADS;
+    using v4 = __attribute__((ext_vector_type(4))) unsigned int;
+    const v4* A = reinterpret_cast<const v4*>(algo);
+    const v4* R = reinterpret_cast<const v4*>(real);
+    for (int64_t k = (int64_t)blockIdx.x * SCORE_THREADS + threadIdx.x; k < nv; k += stride) {
+        const v4 a = __builtin_nontemporal_load(A + k), r = __builtin_nontemporal_load(R + k);
+        score_one(a.x, r.x, parent, depth, c);
+        score_one(a.y, r.y, parent, depth, c);
+        score_one(a.z, r.z, parent, depth, c);
+        score_one(a.w, r.w, parent, depth, c);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) score_one(algo[4 * nv + threadIdx.x], real[4 * nv + threadIdx.x], parent, depth, c);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        unsigned long long v = c[q];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(counts + q, v);
+    }
+}
+
 __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint64_t n, uint64_t seed, int mode) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
@@ -755,6 +804,17 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         hipLaunchKernelGGL(dfa_scan_kernel<2>, g, b, 0, s, text, stream_start, pos0, n, out, count, t, seg);
     else
         hipLaunchKernelGGL(dfa_scan_kernel<0>, g, b, 0, s, text, stream_start, pos0, n, out, count, t, seg);
+    return hipGetLastError();
+}
+
+hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,
+                          const uint32_t* depth, unsigned long long* counts, int num_cu, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n / 4 + SCORE_THREADS - 1) / SCORE_THREADS;
+    if (blocks > (int64_t)num_cu * 8) blocks = (int64_t)num_cu * 8;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(score_kernel, dim3((unsigned)blocks), dim3(SCORE_THREADS), 0, s, algo, real, n, parent, depth,
+                       counts);
     return hipGetLastError();
 }
 

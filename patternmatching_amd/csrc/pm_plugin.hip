@@ -62,6 +62,9 @@ struct PmHip {
     // device tables
     RtDev rt{};
     DfaDev dfa{};
+    const uint32_t* d_parent = nullptr;  // PmParents, gid space (scoring)
+    const uint32_t* d_depth = nullptr;
+    std::vector<uint32_t> parent;
     std::vector<void*> allocs;
     size_t table_bytes = 0;
     // streaming
@@ -214,6 +217,12 @@ void pm_hip_compile(void* obj) {
             o->kind = KIND_AC;
         }
     }
+    {
+        PmParents par = pm_build_parents(o->pats, o->gids);
+        o->d_parent = (const uint32_t*)dalloc_copy(o, par.parent.data(), par.parent.size() * 4);
+        o->d_depth = (const uint32_t*)dalloc_copy(o, par.depth.data(), par.depth.size() * 4);
+        o->parent = std::move(par.parent);
+    }
     if (o->kind == KIND_AC) {
         DfaImage im = pm_build_dfa(o->pats, o->gids);
         o->dfa.next = (const uint32_t*)dalloc_copy(o, im.next.data(), im.next.size() * 4);
@@ -328,6 +337,30 @@ int pm_hip_scan_device16(void* obj, const uint8_t* d_text, int64_t stream_start,
     return scan_device(obj, d_text, stream_start, pos0, n, d_out, 2, d_count, hip_stream);
 }
 
+int pm_hip_score_device(void* obj, const uint32_t* d_algo, const uint32_t* d_real, int64_t n,
+                        unsigned long long* d_counts, void* hip_stream) {
+    PmHip* o = as(obj);
+    if (!o->compiled) { std::snprintf(g_err, sizeof(g_err), "not compiled"); return -1; }
+    if (n < 0 || !d_counts || ((uintptr_t)d_algo & 15) || ((uintptr_t)d_real & 15)) {
+        std::snprintf(g_err, sizeof(g_err), "bad arguments (n >= 0, counts, 16-B alignment)");
+        return -2;
+    }
+    hipError_t e = hipSetDevice(o->device);
+    if (e == hipSuccess)
+        e = pm_launch_score(d_algo, d_real, n, o->d_parent, o->d_depth, d_counts, o->num_cu, (hipStream_t)hip_stream);
+    if (e != hipSuccess) {
+        std::snprintf(g_err, sizeof(g_err), "score launch: %s", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
+}
+
+uint32_t pm_hip_parent_gid(void* obj, uint32_t gid) {
+    PmHip* o = as(obj);
+    if (!o->compiled || gid >= o->parent.size()) return UINT32_MAX;
+    return o->parent[gid];
+}
+
 // Timing-only ablation launches of the RT kernel (bench_variants.py).
 int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out, int out_width,
                               unsigned long long* d_count, void* hip_stream, int blocks) {
@@ -371,6 +404,7 @@ struct PmFlatHandle {
     PmGidMap g;
     RtImage rt;
     DfaImage dfa;
+    PmParents par;
     int kind = 0;
 };
 }  // namespace
@@ -386,6 +420,7 @@ void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int
     h->g = pm_assign_gids(v);
     if (kind == KIND_RT) h->rt = pm_build_rt(v, h->g);
     else h->dfa = pm_build_dfa(v, h->g);
+    h->par = pm_build_parents(v, h->g);
     return h;
 }
 
@@ -406,6 +441,8 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
     if (s == "next") return ret(h->dfa.next);
     if (s == "out") return ret(h->dfa.out);
     if (s == "index_of_gid") return ret(h->g.index_of_gid);
+    if (s == "parent") return ret(h->par.parent);
+    if (s == "depth") return ret(h->par.depth);
     *data = nullptr;
     *elem_size = 0;
     return 0;

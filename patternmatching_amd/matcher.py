@@ -177,6 +177,16 @@ class HipMatcher:
         if rc != 0:
             raise RuntimeError(self.lib.pm_hip_last_error().decode())
 
+    def score_device(self, d_algo_ptr, d_real_ptr, n, d_counts_ptr, stream_ptr):
+        """pm_hip_score_device: d_counts (5 u64) += success, partial,
+        false_neg, false_pos, all_matches of algo ids against real ids."""
+        rc = self.lib.pm_hip_score_device(self.obj, d_algo_ptr, d_real_ptr, n, d_counts_ptr, stream_ptr)
+        if rc != 0:
+            raise RuntimeError(self.lib.pm_hip_last_error().decode())
+
+    def parent_gid(self, gid):
+        return self.lib.pm_hip_parent_gid(self.obj, gid)
+
     @property
     def kernel_kind(self):
         return self.lib.pm_hip_kernel_kind(self.obj)

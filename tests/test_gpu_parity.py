@@ -299,6 +299,72 @@ def test_u16_ids_refused_for_large_dictionaries():
                       out_width=2)
 
 
+def _score_host(algo, real, parent, depth):
+    """measure_success_rate (Core/src/measure.c:174-190) + all-matches, numpy."""
+    algo = algo.astype(np.int64)
+    real = real.astype(np.int64)
+    eq = algo == real
+    fn = ~eq & (algo == 0)
+    part = 0
+    for i in np.nonzero(~eq & (algo != 0))[0]:
+        cur = real[i]
+        while cur and cur != algo[i]:
+            cur = parent[cur]
+        part += cur != 0
+    fp = int(np.count_nonzero(~eq & (algo != 0))) - part
+    return [int(eq.sum()), part, int(fn.sum()), fp, int(depth[real].sum())]
+
+
+@pytest.mark.parametrize("key", ["snort", "merged"])
+def test_score_device_matches_measure_success_rate(key):
+    """pm_hip_score_device == the reference's scoring (numpy restatement over
+    the patterns-tree parents) on RT vs AC ids (all success) and on ids with
+    injected partial / false-negative / false-positive answers."""
+    torch = _torch()
+    s = torch.cuda.current_stream().cuda_stream
+    rt, ac = matcher(key, "rt"), matcher(key, "ac")
+    n = (4 << 20) + 12
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    pm.load().pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 21, 0, s)
+    a = torch.empty(n + 4, dtype=torch.int32, device="cuda")
+    b = torch.empty(n + 4, dtype=torch.int32, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), None, s)
+    ac.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), None, s)
+    torch.cuda.synchronize()
+    P = rt.lib.pm_hip_n_patterns(rt.obj)
+    parent = np.array([rt.parent_gid(g) for g in range(P + 1)], np.int64)
+    depth = np.zeros(P + 1, np.int64)
+    for g in range(1, P + 1):  # patterns on g's suffix chain, g included
+        c, k = g, 0
+        while c:
+            c, k = parent[c], k + 1
+        depth[g] = k
+    real = b[:n].cpu().numpy().view(np.uint32)
+    cnt = torch.zeros(5, dtype=torch.int64, device="cuda")
+    rt.score_device(a.data_ptr(), b.data_ptr(), n, cnt.data_ptr(), s)
+    torch.cuda.synchronize()
+    exp = _score_host(a[:n].cpu().numpy().view(np.uint32), real, parent, depth)
+    assert cnt.cpu().tolist() == exp and exp[0] == n
+    # injected errors: partial (a proper suffix pattern), false negatives, false positives
+    algo = real.copy()
+    rng = np.random.default_rng(3)
+    withpar = np.nonzero(parent[real] > 0)[0]
+    sel = rng.choice(withpar, 5000, replace=False)
+    algo[sel] = parent[real[sel]]
+    nz = np.nonzero(real)[0]
+    algo[rng.choice(nz, 4000, replace=False)] = 0
+    fpi = rng.choice(n, 3000, replace=False)
+    algo[fpi] = rng.integers(1, P + 1, 3000)
+    ad = torch.from_numpy(np.concatenate([algo, np.zeros(4, np.uint32)]).view(np.int32)).cuda()
+    cnt.zero_()
+    rt.score_device(ad.data_ptr(), b.data_ptr(), n, cnt.data_ptr(), s)
+    torch.cuda.synchronize()
+    exp = _score_host(algo, real, parent, depth)
+    got = cnt.cpu().tolist()
+    assert got == exp, (got, exp)
+    assert exp[1] > 1000 and exp[2] > 1000 and exp[3] > 1000
+
+
 @pytest.mark.slow
 def test_full_size_snort_1gib_kernels_agree():
     """BASELINE config 3 size (snort, 1 GiB): the two independent kernels agree

@@ -101,6 +101,26 @@ def test_rt_stage2_filter_keeps_every_answer_changing_suffix(key):
     assert stage2.sum() < 0.55 * stage1.sum(), (stage2.sum(), stage1.sum())
 
 
+@pytest.mark.parametrize("key", ["et", "snort", "merged"])
+def test_parent_and_depth_tables_follow_the_patterns_tree(key):
+    """pm_build_parents (gid space) == the host patterns tree's parent
+    (pm_dict, the reference's longest-proper-suffix-pattern tree), and depth
+    = 1 + depth(parent)."""
+    d, img, _ = image(key, pm.KIND_RT)
+    idx = img.array("index_of_gid").astype(np.int64)
+    parent = img.array("parent").astype(np.int64)
+    depth = img.array("depth").astype(np.int64)
+    P = len(idx) - 1
+    gid_of = np.zeros(P, np.int64)
+    gid_of[idx[1:]] = np.arange(1, P + 1)
+    host = d.parents()  # pattern index -> parent index, -1 = none
+    exp = np.where(host[idx[1:]] >= 0, gid_of[np.maximum(host[idx[1:]], 0)], 0)
+    assert np.array_equal(parent[1:], exp)
+    assert parent[0] == 0 and depth[0] == 0
+    assert np.array_equal(depth[1:], 1 + np.where(parent[1:] > 0, depth[parent[1:]], 0))
+    assert depth.max() >= 3
+
+
 def test_rt_image_context():
     """Positions scanned with only max_len-1 bytes of context are exact."""
     d, img, tab = image("merged", pm.KIND_RT)
