@@ -186,6 +186,14 @@ def main():
                                  "false_pos_rate": c[3] / n, "false_neg_rate": c[2] / n, "partial_rate": c[1] / n,
                                  "score_ms": round(e0.elapsed_time(e1), 4)}
             del ref
+            hist = torch.zeros(lib.pm_hip_n_patterns(m.obj) + 1, dtype=torch.int64, device="cuda")
+            e0.record(stream)
+            m.pattern_counts_device(out.data_ptr(), n, hist.data_ptr(), stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            extra["pattern_counts"] = {"patterns_seen": int((hist > 0).sum().item()),
+                                       "occurrences": int(hist.sum().item()),
+                                       "ms": round(e0.elapsed_time(e1), 4)}
         if use_dist:
             dist.all_reduce(allm, op=dist.ReduceOp.SUM)
         extra["all_matches_per_step"] = int(allm[4].item())

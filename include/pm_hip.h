@@ -97,6 +97,12 @@ int pm_hip_scan_device16(void* obj, const uint8_t* d_text, int64_t stream_start,
  * Asynchronous. */
 int pm_hip_score_device(void* obj, const uint32_t* d_algo, const uint32_t* d_real, int64_t n,
                         unsigned long long* d_counts, void* hip_stream);
+/* Per-pattern occurrence counts of a dense u32 gid stream (all-matches
+ * expansion: each position counts its answer and every pattern on the
+ * answer's suffix chain).  d_hist: n_patterns + 1 device u64, indexed by gid
+ * (pm_hip_gid_index maps a gid to its add order), accumulated.  Asynchronous. */
+int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, unsigned long long* d_hist,
+                                 void* hip_stream);
 /* The patterns-tree parent of a gid (longest proper suffix pattern, 0 = none);
  * UINT32_MAX when out of range. */
 uint32_t pm_hip_parent_gid(void* obj, uint32_t gid);

@@ -88,6 +88,7 @@ SIGNATURES = {
                                             c_vp, c_vp]),
     "pm_hip_score_device": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, c_vp, c_vp]),
     "pm_hip_parent_gid": (ctypes.c_uint32, [c_vp, ctypes.c_uint32]),
+    "pm_hip_pattern_counts_device": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, c_vp, c_vp]),
     "pm_hip_gen_stream_device": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_int, c_vp]),
     "pm_gen_stream_host": (None, [c_u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),

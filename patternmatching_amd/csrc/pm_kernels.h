@@ -35,4 +35,8 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 // against real (n u32 gids each, 16-B aligned); parent/depth: PmParents.
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,
                           const uint32_t* depth, unsigned long long* counts, int num_cu, hipStream_t s);
+// hist[g] (u64, g in 1..n_gids-1) += occurrences of pattern g in the stream
+// whose dense answers are real: the suffix chain of every answer.
+hipError_t pm_launch_pattern_counts(const uint32_t* real, int64_t n, const uint32_t* parent, uint32_t n_gids,
+                                   unsigned long long* hist, int num_cu, hipStream_t s);
 hipError_t pm_launch_gen(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode, hipStream_t s);

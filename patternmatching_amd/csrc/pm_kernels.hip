@@ -717,6 +717,41 @@ __global__ __launch_bounds__(SCORE_THREADS) void score_kernel(const uint32_t* __
     }
 }
 
+// Per-pattern occurrence counts: every pattern on the suffix chain of
+// real[i] occurs at i (all-matches expansion).  Gids [lo, lo + cnt) are
+// counted in an LDS histogram per workgroup (cnt <= HIST_WINDOW), flushed to
+// the u64 global histogram (nonzero counters only) at the end.
+constexpr int HIST_THREADS = 1024;
+constexpr uint32_t HIST_WINDOW = 38912;  // 152 KiB of u32 counters
+
+__global__ __launch_bounds__(HIST_THREADS) void hist_kernel(const uint32_t* __restrict__ real, int64_t n,
+                                                            const uint32_t* __restrict__ parent, uint32_t lo,
+                                                            uint32_t cnt, unsigned long long* __restrict__ hist) {
+    __shared__ uint32_t s_h[HIST_WINDOW];
+    for (uint32_t k = threadIdx.x; k < cnt; k += HIST_THREADS) s_h[k] = 0;
+    __syncthreads();
+    auto add = [&](uint32_t g) {
+        while (g) {
+            if (g - lo < cnt) atomicAdd(&s_h[g - lo], 1u);
+            g = parent[g];
+        }
+    };
+    using v4 = __attribute__((ext_vector_type(4))) unsigned int;
+    const int64_t nv = n / 4;
+    const int64_t stride = (int64_t)gridDim.x * HIST_THREADS;
+    for (int64_t k = (int64_t)blockIdx.x * HIST_THREADS + threadIdx.x; k < nv; k += stride) {
+        const v4 r = __builtin_nontemporal_load(reinterpret_cast<const v4*>(real) + k);
+        add(r.x);
+        add(r.y);
+        add(r.z);
+        add(r.w);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) add(real[4 * nv + threadIdx.x]);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < cnt; k += HIST_THREADS)
+        if (s_h[k]) atomicAdd(hist + lo + k, (unsigned long long)s_h[k]);
+}
+
 __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint64_t n, uint64_t seed, int mode) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
@@ -816,6 +851,21 @@ hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n
     hipLaunchKernelGGL(score_kernel, dim3((unsigned)blocks), dim3(SCORE_THREADS), 0, s, algo, real, n, parent, depth,
                        counts);
     return hipGetLastError();
+}
+
+hipError_t pm_launch_pattern_counts(const uint32_t* real, int64_t n, const uint32_t* parent, uint32_t n_gids,
+                                   unsigned long long* hist, int num_cu, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n / 4 + HIST_THREADS - 1) / HIST_THREADS;
+    if (blocks > num_cu) blocks = num_cu;  // one workgroup per CU (LDS-bound)
+    if (blocks < 1) blocks = 1;
+    for (uint32_t lo = 1; lo < n_gids; lo += HIST_WINDOW) {
+        const uint32_t cnt = n_gids - lo < HIST_WINDOW ? n_gids - lo : HIST_WINDOW;
+        hipLaunchKernelGGL(hist_kernel, dim3((unsigned)blocks), dim3(HIST_THREADS), 0, s, real, n, parent, lo, cnt, hist);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t pm_launch_gen(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode, hipStream_t s) {

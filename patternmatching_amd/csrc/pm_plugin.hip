@@ -355,6 +355,25 @@ int pm_hip_score_device(void* obj, const uint32_t* d_algo, const uint32_t* d_rea
     return 0;
 }
 
+int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, unsigned long long* d_hist,
+                                 void* hip_stream) {
+    PmHip* o = as(obj);
+    if (!o->compiled) { std::snprintf(g_err, sizeof(g_err), "not compiled"); return -1; }
+    if (n < 0 || !d_hist || ((uintptr_t)d_ids & 15)) {
+        std::snprintf(g_err, sizeof(g_err), "bad arguments (n >= 0, hist, 16-B alignment)");
+        return -2;
+    }
+    hipError_t e = hipSetDevice(o->device);
+    if (e == hipSuccess)
+        e = pm_launch_pattern_counts(d_ids, n, o->d_parent, (uint32_t)o->parent.size(), d_hist, o->num_cu,
+                                     (hipStream_t)hip_stream);
+    if (e != hipSuccess) {
+        std::snprintf(g_err, sizeof(g_err), "pattern counts launch: %s", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
+}
+
 uint32_t pm_hip_parent_gid(void* obj, uint32_t gid) {
     PmHip* o = as(obj);
     if (!o->compiled || gid >= o->parent.size()) return UINT32_MAX;

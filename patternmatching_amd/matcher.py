@@ -184,6 +184,13 @@ class HipMatcher:
         if rc != 0:
             raise RuntimeError(self.lib.pm_hip_last_error().decode())
 
+    def pattern_counts_device(self, d_ids_ptr, n, d_hist_ptr, stream_ptr):
+        """pm_hip_pattern_counts_device: d_hist (u64[n_patterns + 1], by gid)
+        += occurrences of every pattern (suffix chains of the dense ids)."""
+        rc = self.lib.pm_hip_pattern_counts_device(self.obj, d_ids_ptr, n, d_hist_ptr, stream_ptr)
+        if rc != 0:
+            raise RuntimeError(self.lib.pm_hip_last_error().decode())
+
     def parent_gid(self, gid):
         return self.lib.pm_hip_parent_gid(self.obj, gid)
 

@@ -365,6 +365,34 @@ def test_score_device_matches_measure_success_rate(key):
     assert exp[1] > 1000 and exp[2] > 1000 and exp[3] > 1000
 
 
+@pytest.mark.parametrize("key", ["snort", "merged"])
+def test_pattern_counts_device(key):
+    """pm_hip_pattern_counts_device == numpy all-matches expansion over the
+    parent chains (merged needs two LDS windows of gids)."""
+    torch = _torch()
+    s = torch.cuda.current_stream().cuda_stream
+    rt = matcher(key, "rt")
+    n = (2 << 20) + 7
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    pm.load().pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 23, 0, s)
+    ids = torch.empty(n + 4, dtype=torch.int32, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, ids.data_ptr(), None, s)
+    P = rt.lib.pm_hip_n_patterns(rt.obj)
+    hist = torch.zeros(P + 1, dtype=torch.int64, device="cuda")
+    rt.pattern_counts_device(ids.data_ptr(), n, hist.data_ptr(), s)
+    torch.cuda.synchronize()
+    parent = np.array([rt.parent_gid(g) for g in range(P + 1)], np.int64)
+    exp = np.zeros(P + 1, np.int64)
+    cur = ids[:n].cpu().numpy().view(np.uint32).astype(np.int64)
+    while cur.any():
+        cur = cur[cur > 0]
+        np.add.at(exp, cur, 1)
+        cur = parent[cur]
+    got = hist.cpu().numpy()
+    assert np.array_equal(got, exp)
+    assert got.sum() > n // 2 and (got > 0).sum() > 1000
+
+
 @pytest.mark.slow
 def test_full_size_snort_1gib_kernels_agree():
     """BASELINE config 3 size (snort, 1 GiB): the two independent kernels agree
