@@ -103,6 +103,13 @@ int pm_hip_score_device(void* obj, const uint32_t* d_algo, const uint32_t* d_rea
  * (pm_hip_gid_index maps a gid to its add order), accumulated.  Asynchronous. */
 int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, unsigned long long* d_hist,
                                  void* hip_stream);
+/* Compiled-image cache: compile() keeps the flattened tables of each
+ * dictionary in DIR (pm-<kind>-<hash>.img, keyed by the patterns in add order)
+ * and reuses them; without a call here, $PM_IMAGE_CACHE names the directory
+ * (unset = no cache).  A file that does not validate is rebuilt. */
+void pm_hip_set_image_cache(void* obj, const char* dir);
+/* 1 when the last compile() loaded its tables from the cache. */
+int pm_hip_image_cache_hit(void* obj);
 /* The patterns-tree parent of a gid (longest proper suffix pattern, 0 = none);
  * UINT32_MAX when out of range. */
 uint32_t pm_hip_parent_gid(void* obj, uint32_t gid);
@@ -141,6 +148,9 @@ int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int
  *         to check the flattener, and by DESIGN.md sizing) ------------ */
 /* kind 1 = reverse-trie image, 2 = AC dense-DFA image */
 void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int kind);
+/* The same through the compiled-image cache in cache_dir (NULL = none). */
+void* pm_flat_build_cached(const char* const* pats, const uint32_t* lens, size_t n, int kind, const char* cache_dir);
+int pm_flat_cache_hit(void* handle);
 int pm_flat_fits(void* handle);
 /* name: "t12" "filt" "n2i" "t3" "rec" "next" "out" "index_of_gid"; returns element count */
 size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* elem_size);

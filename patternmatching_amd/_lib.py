@@ -88,6 +88,8 @@ SIGNATURES = {
                                             c_vp, c_vp]),
     "pm_hip_score_device": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, c_vp, c_vp]),
     "pm_hip_parent_gid": (ctypes.c_uint32, [c_vp, ctypes.c_uint32]),
+    "pm_hip_set_image_cache": (None, [c_vp, ctypes.c_char_p]),
+    "pm_hip_image_cache_hit": (ctypes.c_int, [c_vp]),
     "pm_hip_pattern_counts_device": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, c_vp, c_vp]),
     "pm_hip_gen_stream_device": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_int, c_vp]),
@@ -105,6 +107,9 @@ SIGNATURES = {
                                                  c_vp, c_vp, ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
+    "pm_flat_build_cached": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int,
+                                    ctypes.c_char_p]),
+    "pm_flat_cache_hit": (ctypes.c_int, [c_vp]),
     "pm_flat_fits": (ctypes.c_int, [c_vp]),
     "pm_flat_array": (ctypes.c_size_t, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
                                         ctypes.POINTER(ctypes.c_size_t)]),

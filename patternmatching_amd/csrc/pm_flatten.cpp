@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdio>
+#include <unistd.h>
 #include <cstring>
 #include <unordered_map>
 
@@ -278,5 +280,124 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
         // suffix link / output (mpac.c:179, :318)
         im.out[v] = v == 0 ? 0 : (t.gid[v] ? t.gid[v] : im.out[fail[v]]);
     }
+    return im;
+}
+
+// ---- compiled-image cache --------------------------------------------------
+
+namespace {
+
+constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
+constexpr uint32_t IMG_VERSION = 3;                     // bump when a table layout changes
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001B3ull;
+    return h;
+}
+
+template <class T>
+bool put(FILE* f, uint32_t tag, const std::vector<T>& v) {
+    const uint32_t es = sizeof(T);
+    const uint64_t n = v.size();
+    return std::fwrite(&tag, 4, 1, f) == 1 && std::fwrite(&es, 4, 1, f) == 1 && std::fwrite(&n, 8, 1, f) == 1 &&
+           (n == 0 || std::fwrite(v.data(), es, n, f) == n);
+}
+
+template <class T>
+bool get(FILE* f, uint32_t tag, std::vector<T>& v) {
+    uint32_t t = 0, es = 0;
+    uint64_t n = 0;
+    if (std::fread(&t, 4, 1, f) != 1 || std::fread(&es, 4, 1, f) != 1 || std::fread(&n, 8, 1, f) != 1) return false;
+    if (t != tag || es != sizeof(T) || n > ((uint64_t)1 << 36) / es) return false;
+    v.resize(n);
+    return n == 0 || std::fread(v.data(), es, n, f) == n;
+}
+
+bool save(const std::string& path, uint64_t key, int kind, const PmImages& im) {
+    const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return false;
+    const uint32_t hdr[2] = {IMG_VERSION, (uint32_t)kind};
+    const std::vector<uint32_t> scal = {im.rt.fits ? 1u : 0u, im.rt.t3h_bits, im.rt.n2int, im.rt.nrec, im.rt.nodes,
+                                        im.rt.d3, im.dfa.states};
+    bool ok = std::fwrite(&IMG_MAGIC, 8, 1, f) == 1 && std::fwrite(&key, 8, 1, f) == 1 && std::fwrite(hdr, 4, 2, f) == 2 &&
+              put(f, 1, scal) && put(f, 2, im.rt.t12) && put(f, 3, im.rt.filt) && put(f, 4, im.rt.t3h) &&
+              put(f, 5, im.rt.rec) && put(f, 6, im.dfa.next) && put(f, 7, im.dfa.out) && put(f, 8, im.par.parent) &&
+              put(f, 9, im.par.depth);
+    ok = (std::fclose(f) == 0) && ok;
+    if (ok) ok = std::rename(tmp.c_str(), path.c_str()) == 0;
+    if (!ok) std::remove(tmp.c_str());
+    return ok;
+}
+
+bool load(const std::string& path, uint64_t key, int kind, PmImages& im) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    uint64_t magic = 0, k = 0;
+    uint32_t hdr[2] = {0, 0};
+    std::vector<uint32_t> scal;
+    bool ok = std::fread(&magic, 8, 1, f) == 1 && std::fread(&k, 8, 1, f) == 1 && std::fread(hdr, 4, 2, f) == 2 &&
+              magic == IMG_MAGIC && k == key && hdr[0] == IMG_VERSION && hdr[1] == (uint32_t)kind &&
+              get(f, 1, scal) && scal.size() == 7 && get(f, 2, im.rt.t12) && get(f, 3, im.rt.filt) &&
+              get(f, 4, im.rt.t3h) && get(f, 5, im.rt.rec) && get(f, 6, im.dfa.next) && get(f, 7, im.dfa.out) &&
+              get(f, 8, im.par.parent) && get(f, 9, im.par.depth);
+    char extra;
+    ok = ok && std::fread(&extra, 1, 1, f) == 0;  // nothing after the last section
+    std::fclose(f);
+    if (!ok) return false;
+    im.rt.fits = scal[0] != 0;
+    im.rt.t3h_bits = scal[1];
+    im.rt.n2int = scal[2];
+    im.rt.nrec = scal[3];
+    im.rt.nodes = scal[4];
+    im.rt.d3 = scal[5];
+    im.dfa.states = scal[6];
+    // structural checks: the kernels index these tables without bounds
+    if (kind == 1 && im.rt.fits &&
+        (im.rt.t12.size() != RT_T1_BASE + 256 || im.rt.filt.size() != RT_FILTER_WORDS + RT_F2_WORDS ||
+         im.rt.t3h_bits < 4 || im.rt.t3h_bits > 30 || im.rt.t3h.size() != ((size_t)4 << im.rt.t3h_bits) ||
+         im.rt.rec.size() != (size_t)im.rt.nrec * RT_REC_WORDS))
+        return false;
+    if (kind == 2 && (im.dfa.next.size() != (size_t)im.dfa.states * 256 || im.dfa.out.size() != im.dfa.states))
+        return false;
+    return true;
+}
+
+}  // namespace
+
+uint64_t pm_image_key(const std::vector<std::string>& pats, int kind) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    const uint32_t v[2] = {IMG_VERSION, (uint32_t)kind};
+    h = fnv1a(h, v, sizeof v);
+    for (const auto& p : pats) {
+        const uint64_t n = p.size();
+        h = fnv1a(h, &n, 8);
+        h = fnv1a(h, p.data(), p.size());
+    }
+    return h;
+}
+
+PmImages pm_build_images_cached(const std::vector<std::string>& pats, const PmGidMap& g, int kind,
+                                const std::string& dir, bool* hit) {
+    PmImages im;
+    *hit = false;
+    std::string path;
+    uint64_t key = 0;
+    if (!dir.empty()) {
+        key = pm_image_key(pats, kind);
+        char name[64];
+        std::snprintf(name, sizeof name, "/pm-%d-%016llx.img", kind, (unsigned long long)key);
+        path = dir + name;
+        if (load(path, key, kind, im) && im.par.parent.size() == g.index_of_gid.size()) {
+            *hit = true;
+            return im;
+        }
+        im = PmImages();
+    }
+    if (kind == 1) im.rt = pm_build_rt(pats, g);
+    else im.dfa = pm_build_dfa(pats, g);
+    im.par = pm_build_parents(pats, g);
+    if (!dir.empty()) save(path, key, kind, im);  // best effort
     return im;
 }

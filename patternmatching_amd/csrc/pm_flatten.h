@@ -94,6 +94,23 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g);
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g);
 PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap& g);
 
+// Compiled-image cache: the flattened tables of a
+// dictionary, on disk, keyed by a hash of the patterns in add order and the
+// image kind.  pm_image_key hashes (format version, kind, every pattern's
+// length and bytes).  Files are written to a temporary name and renamed, so
+// a reader never sees a partial file; anything that does not validate
+// (magic, key, kind, section sizes) is ignored and rebuilt.
+struct PmImages {
+    RtImage rt;
+    DfaImage dfa;
+    PmParents par;
+};
+uint64_t pm_image_key(const std::vector<std::string>& pats, int kind);
+// Build (kind 1 = RT, 2 = DFA; parents always), through the cache directory
+// when dir is non-empty.  *hit tells whether the file was used.
+PmImages pm_build_images_cached(const std::vector<std::string>& pats, const PmGidMap& g, int kind,
+                                const std::string& dir, bool* hit);
+
 constexpr uint32_t RT_T1_BASE = 65536;   // t12[65536 + c]: lookback of exactly one byte
 constexpr uint32_t RT_CONT16 = 0x8000u;  // t12: depth-2 node has children (low 15 bits: best so far)
 constexpr uint32_t RT_CONT32 = 0x80000000u;  // t3: continue at record (low 31 bits)

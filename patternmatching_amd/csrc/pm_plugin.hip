@@ -65,6 +65,8 @@ struct PmHip {
     const uint32_t* d_parent = nullptr;  // PmParents, gid space (scoring)
     const uint32_t* d_depth = nullptr;
     std::vector<uint32_t> parent;
+    std::string cache_dir;   // compiled-image cache (else $PM_IMAGE_CACHE)
+    bool cache_hit = false;
     std::vector<void*> allocs;
     size_t table_bytes = 0;
     // streaming
@@ -202,33 +204,33 @@ void pm_hip_compile(void* obj) {
     PM_CHECK(hipSetDevice(o->device));
     o->gids = pm_assign_gids(o->pats);
     o->kind = o->kind_req;
+    // flattened tables, through the on-disk image cache when configured
+    const char* env = std::getenv("PM_IMAGE_CACHE");
+    const std::string dir = !o->cache_dir.empty() ? o->cache_dir : (env ? env : "");
+    bool hit = false;
+    PmImages im = pm_build_images_cached(o->pats, o->gids, o->kind, dir, &hit);
+    if (o->kind == KIND_RT && !im.rt.fits) {
+        std::fprintf(stderr, "pm_hip: dictionary exceeds the reverse-trie u16 encoding; using the DFA kernel\n");
+        o->kind = KIND_AC;
+        im = pm_build_images_cached(o->pats, o->gids, o->kind, dir, &hit);
+    }
+    o->cache_hit = hit;
     if (o->kind == KIND_RT) {
-        RtImage im = pm_build_rt(o->pats, o->gids);
-        if (im.fits) {
-            o->rt.t12 = (const uint16_t*)dalloc_copy(o, im.t12.data(), im.t12.size() * 2);
-            o->rt.filt = (const uint32_t*)dalloc_copy(o, im.filt.data(), im.filt.size() * 4);
-            o->rt.t3h = (const uint4*)dalloc_copy(o, im.t3h.data(), im.t3h.size() * 4);
-            o->rt.t3h_bits = im.t3h_bits;
-            o->rt.rec = (const uint32_t*)dalloc_copy(o, im.rec.data(), im.rec.size() * 4);
-            const std::vector<uint8_t> zero(RT_SCRATCH_BYTES, 0);
-            o->rt.scratch = (uint32_t*)dalloc_copy(o, zero.data(), zero.size());
-        } else {
-            std::fprintf(stderr, "pm_hip: dictionary exceeds the reverse-trie u16 encoding; using the DFA kernel\n");
-            o->kind = KIND_AC;
-        }
-    }
-    {
-        PmParents par = pm_build_parents(o->pats, o->gids);
-        o->d_parent = (const uint32_t*)dalloc_copy(o, par.parent.data(), par.parent.size() * 4);
-        o->d_depth = (const uint32_t*)dalloc_copy(o, par.depth.data(), par.depth.size() * 4);
-        o->parent = std::move(par.parent);
-    }
-    if (o->kind == KIND_AC) {
-        DfaImage im = pm_build_dfa(o->pats, o->gids);
-        o->dfa.next = (const uint32_t*)dalloc_copy(o, im.next.data(), im.next.size() * 4);
-        o->dfa.out = (const uint32_t*)dalloc_copy(o, im.out.data(), im.out.size() * 4);
+        o->rt.t12 = (const uint16_t*)dalloc_copy(o, im.rt.t12.data(), im.rt.t12.size() * 2);
+        o->rt.filt = (const uint32_t*)dalloc_copy(o, im.rt.filt.data(), im.rt.filt.size() * 4);
+        o->rt.t3h = (const uint4*)dalloc_copy(o, im.rt.t3h.data(), im.rt.t3h.size() * 4);
+        o->rt.t3h_bits = im.rt.t3h_bits;
+        o->rt.rec = (const uint32_t*)dalloc_copy(o, im.rt.rec.data(), im.rt.rec.size() * 4);
+        const std::vector<uint8_t> zero(RT_SCRATCH_BYTES, 0);
+        o->rt.scratch = (uint32_t*)dalloc_copy(o, zero.data(), zero.size());
+    } else {
+        o->dfa.next = (const uint32_t*)dalloc_copy(o, im.dfa.next.data(), im.dfa.next.size() * 4);
+        o->dfa.out = (const uint32_t*)dalloc_copy(o, im.dfa.out.data(), im.dfa.out.size() * 4);
         o->dfa.warm = o->max_len ? (int64_t)o->max_len - 1 : 0;
     }
+    o->d_parent = (const uint32_t*)dalloc_copy(o, im.par.parent.data(), im.par.parent.size() * 4);
+    o->d_depth = (const uint32_t*)dalloc_copy(o, im.par.depth.data(), im.par.depth.size() * 4);
+    o->parent = std::move(im.par.parent);
     PM_CHECK(hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking));
     PM_CHECK(hipEventCreate(&o->ev0));
     PM_CHECK(hipEventCreate(&o->ev1));
@@ -374,6 +376,10 @@ int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, un
     return 0;
 }
 
+void pm_hip_set_image_cache(void* obj, const char* dir) { as(obj)->cache_dir = dir ? dir : ""; }
+
+int pm_hip_image_cache_hit(void* obj) { return as(obj)->cache_hit ? 1 : 0; }
+
 uint32_t pm_hip_parent_gid(void* obj, uint32_t gid) {
     PmHip* o = as(obj);
     if (!o->compiled || gid >= o->parent.size()) return UINT32_MAX;
@@ -425,23 +431,31 @@ struct PmFlatHandle {
     DfaImage dfa;
     PmParents par;
     int kind = 0;
+    bool hit = false;
 };
 }  // namespace
 
 extern "C" {
 
-void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int kind) {
+void* pm_flat_build_cached(const char* const* pats, const uint32_t* lens, size_t n, int kind, const char* cache_dir) {
     std::vector<std::string> v;
     v.reserve(n);
     for (size_t i = 0; i < n; ++i) v.emplace_back(pats[i], lens[i]);
     PmFlatHandle* h = new PmFlatHandle();
     h->kind = kind;
     h->g = pm_assign_gids(v);
-    if (kind == KIND_RT) h->rt = pm_build_rt(v, h->g);
-    else h->dfa = pm_build_dfa(v, h->g);
-    h->par = pm_build_parents(v, h->g);
+    PmImages im = pm_build_images_cached(v, h->g, kind, cache_dir ? cache_dir : "", &h->hit);
+    h->rt = std::move(im.rt);
+    h->dfa = std::move(im.dfa);
+    h->par = std::move(im.par);
     return h;
 }
+
+void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int kind) {
+    return pm_flat_build_cached(pats, lens, n, kind, nullptr);
+}
+
+int pm_flat_cache_hit(void* handle) { return static_cast<PmFlatHandle*>(handle)->hit ? 1 : 0; }
 
 int pm_flat_fits(void* handle) { return static_cast<PmFlatHandle*>(handle)->rt.fits ? 1 : 0; }
 

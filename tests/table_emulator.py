@@ -10,13 +10,17 @@ import patternmatching_amd as pm
 
 
 class FlatImage:
-    def __init__(self, patterns, kind):
+    def __init__(self, patterns, kind, cache_dir=None):
         self.lib = pm.load()
         n = len(patterns)
         arr = (ctypes.c_char_p * n)(*patterns)
         lens = (ctypes.c_uint32 * n)(*[len(p) for p in patterns])
-        self.h = self.lib.pm_flat_build(arr, lens, n, kind)
+        if cache_dir is None:
+            self.h = self.lib.pm_flat_build(arr, lens, n, kind)
+        else:
+            self.h = self.lib.pm_flat_build_cached(arr, lens, n, kind, str(cache_dir).encode())
         self.kind = kind
+        self.cache_hit = bool(self.lib.pm_flat_cache_hit(self.h))
 
     def fits(self):
         return bool(self.lib.pm_flat_fits(self.h))

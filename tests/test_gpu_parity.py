@@ -286,6 +286,24 @@ def test_u16_ids_equal_u32_ids(kind):
     assert np.array_equal(m._codes[b.cpu().numpy().view(np.uint16).astype(np.uint32)], exp)
 
 
+def test_image_cache_compile_scans_identically(tmp_path):
+    """compile() through the image cache: the second object loads the file
+    and its scan is identical."""
+    torch = _torch()
+    s = torch.cuda.current_stream().cuda_stream
+    d = pm.Dictionary(dict_paths("snort"))
+    outs = []
+    for k in range(2):
+        m = pm.HipMatcher("rt")
+        m.lib.pm_hip_set_image_cache(m.obj, str(tmp_path).encode())
+        m.add_dictionary(d)
+        m.compile()
+        assert m.lib.pm_hip_image_cache_hit(m.obj) == k
+        text = np.tile(SHIP, 8)
+        outs.append(m.read_block_gids(text))
+    assert np.array_equal(outs[0], outs[1])
+
+
 def test_u16_ids_refused_for_large_dictionaries():
     torch = _torch()
     pats = [b"%05dxq" % k for k in range(70000)]

@@ -121,6 +121,35 @@ def test_parent_and_depth_tables_follow_the_patterns_tree(key):
     assert depth.max() >= 3
 
 
+def test_compiled_image_cache(tmp_path):
+    """miss -> file written; hit -> identical tables; a
+    truncated or foreign file is rebuilt; another dictionary gets its own file."""
+    d = pm.Dictionary(dict_paths("et"))
+    pats = d.patterns()
+    names = {pm.KIND_RT: ["t12", "filt", "t3h", "rec", "parent", "depth"], pm.KIND_AC: ["next", "out", "parent", "depth"]}
+    for kind, arrays in names.items():
+        a = FlatImage(pats, kind, tmp_path)
+        assert not a.cache_hit
+        files = sorted(tmp_path.glob(f"pm-{kind}-*.img"))
+        assert len(files) == 1
+        b = FlatImage(pats, kind, tmp_path)
+        assert b.cache_hit
+        for name in arrays:
+            assert np.array_equal(a.array(name), b.array(name)), name
+        # damage it: truncated, then garbage -> rebuilt and rewritten
+        raw = files[0].read_bytes()
+        files[0].write_bytes(raw[: len(raw) // 2])
+        c = FlatImage(pats, kind, tmp_path)
+        assert not c.cache_hit and np.array_equal(c.array(arrays[0]), a.array(arrays[0]))
+        files[0].write_bytes(b"\0" * 64)
+        assert not FlatImage(pats, kind, tmp_path).cache_hit
+        assert FlatImage(pats, kind, tmp_path).cache_hit
+    e = FlatImage(pats[:-1], pm.KIND_RT, tmp_path)
+    assert not e.cache_hit
+    assert len(list(tmp_path.glob(f"pm-{pm.KIND_RT}-*.img"))) == 2
+    assert not list(tmp_path.glob("*.tmp.*"))
+
+
 def test_rt_image_context():
     """Positions scanned with only max_len-1 bytes of context are exact."""
     d, img, tab = image("merged", pm.KIND_RT)
