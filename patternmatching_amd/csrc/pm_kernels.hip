@@ -47,7 +47,8 @@ constexpr uint32_t RT_POSMASK = (1u << 30) - 1;  // queue item: position - pos0
 constexpr uint32_t RT_SLOT2 = 1u << 30;          // queue item: probe t3h slot2
 
 __device__ __forceinline__ uint32_t rt_hash(uint32_t k) { return k * 0x9E3779B1u; }  // pm_rt_hash
-// pm_rt_fhash: k < 2^24, so this is one full-rate v_mul_u32_u24 (written
+// pm_rt_fhash of the low 24 bits of k (the operand's top byte is ignored):
+// one full-rate v_mul_u32_u24 (written
 // out: the compiler loses the 24-bit range through the byte extraction and
 // would emit the quarter-rate v_mul_lo_u32)
 __device__ __forceinline__ uint32_t rt_fhash(uint32_t k) {
@@ -176,6 +177,8 @@ __device__ uint32_t rt_one(const uint8_t* __restrict__ text, const uint16_t* s_t
 //   5 = product kernel whose round loads all hit one line, 6 = product
 //       kernel without patch stores (both: wrong ids, timing only)
 //  10 = product kernel with sc1 (L2-dropping) chunk stores
+//  11 = t12 + stage-1 filter, no queue; 12 = + queue pushes, no rounds;
+//  13 = 11 + the push's DPP scan only (all: wrong ids, timing only)
 //   9 = product kernel with s_memtime stamps per phase (diagnostic: count
 //       receives 8 u64 cycle sums: lds+filter, push, round wait, consume,
 //       store, issue, chunks, total)
@@ -208,6 +211,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     }
     __syncthreads();
 
+    // ablation phase switches (V = 0: all on)
+    constexpr bool kFilter = V == 0 || V >= 5;
+    constexpr bool kPush = kFilter && V != 11;
+    constexpr bool kRounds = kPush && V != 12 && V != 13;
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -441,7 +448,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         }
         // position j = 4s + b of this lane is pc + 256s + 4*lane + b; its key
         // is the LE u24 ending at byte b of x[s].y (bytes i-2, i-1, i)
-#define RT_KEY(j) ((uint32_t)((((uint64_t)x[(j) >> 2].y << 32) | x[(j) >> 2].x) >> (8 * (2 + ((j) & 3)))) & 0xFFFFFFu)
+#define RT_RAW(j) ((uint32_t)((((uint64_t)x[(j) >> 2].y << 32) | x[(j) >> 2].x) >> (8 * (2 + ((j) & 3)))))
+#define RT_KEY(j) (RT_RAW(j) & 0xFFFFFFu)
         uint32_t res[16];
         uint32_t cm = 0;  // bit j: position j goes past depth 2
 #pragma unroll
@@ -459,14 +467,15 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             }
             res[0] ^= (z == 0x12345u);
         }
-        if (V == 0 || V >= 5) {
+        if (kFilter) {
             uint32_t fw[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) fw[j] = s_f[rt_fhash(RT_KEY(j)) >> 20];
+            for (int j = 0; j < 16; ++j) fw[j] = s_f[rt_fhash(RT_RAW(j)) >> 20];  // the multiply reads 24 bits
 #pragma unroll
-            for (int j = 0; j < 16; ++j) cm |= ((res[j] >> 15) & rt_fhit(fw[j], rt_fhash(RT_KEY(j)))) << j;
+            for (int j = 0; j < 16; ++j) cm |= ((res[j] >> 15) & rt_fhit(fw[j], rt_fhash(RT_RAW(j)))) << j;
         }
 #undef RT_KEY
+#undef RT_RAW
         uint32_t nzm = 0;  // bit j: placeholder j is nonzero
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -475,7 +484,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         }
         cnt += __popc(nzm);
         if (V == 9) { const uint64_t u = stamp(); ph[0] += u - tB; tB = u; }
-        if (V == 0 || V >= 5) {
+        if (V == 11) asm volatile("" ::"v"(cm));  // keeps the filter live
+        if (kRounds) {
             if (rr.n) consume(rr);                      // the round issued last chunk
             if (V == 9) { const uint64_t u = stamp(); ph[3] += u - tB; tB = u; }
             issue(rr, qn >= RT_ROUND ? qn : 0u);  // items of earlier chunks (stores issued)
@@ -509,14 +519,15 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         }
         asm volatile("" ::: "memory");  // the store stays ahead of any later probe
         if (V == 9) { const uint64_t u = stamp(); ph[4] += u - tB; tB = u; }
-        if (V == 0 || V >= 5) {
+        if (kPush) {
             // lane count c = popc(cm); exclusive wave prefix by a DPP scan;
             // items written by a loop over the lane's own set bits
             const uint32_t c = __popc(cm);
             const uint32_t incl = wave_scan_incl(c);
             const uint32_t base = incl - c;
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-            for (uint32_t done = 0;;) {  // wave-uniform
+            if (V == 13) asm volatile("" ::"v"(base), "s"(total));  // ablation: scan only
+            for (uint32_t done = 0; V != 13;) {  // wave-uniform
                 // the in-flight round's possible survivors keep their room
                 const uint32_t room = RT_QCAP - qn - rr.keep;
                 uint32_t mm = cm, rank = base;
@@ -551,6 +562,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 }
             }
             if (V == 9) { const uint64_t u = stamp(); ph[1] += u - tB; tB = u; }
+            if (V == 12) {  // ablation: drop the queue (no rounds)
+                qh += qn;
+                qn = 0;
+            }
         }
         fetch(xr, xp, c + 2 * stride);
     };
@@ -558,10 +573,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // store, prefetch; round, store, prefetch) so the compiler's vmcnt is the
     // steady-state one.
     Round r0;
-    if (V == 0 || V >= 5) issue(r0, 0);
+    if (kRounds) issue(r0, 0);
     stand_in_store();
     fetch(xa, pa, ch);
-    if (V == 0 || V >= 5) issue(rr, 0);
+    if (kRounds) issue(rr, 0);
     stand_in_store();
     fetch(xb, pb, ch + stride);
     for (;;) {  // wave-uniform
@@ -571,7 +586,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         chunk(xb, pb, ch + stride);
         ch += 2 * stride;
     }
-    if (V == 0 || V >= 5) {
+    if (kRounds) {
         if (rr.n) consume(rr);
         while (qn) {  // wave-uniform; every round advances each item
             Round rs;
@@ -800,6 +815,9 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 5: RT_LAUNCH(5); break;
         case 6: RT_LAUNCH(6); break;
         case 10: RT_LAUNCH(10); break;
+        case 11: RT_LAUNCH(11); break;
+        case 12: RT_LAUNCH(12); break;
+        case 13: RT_LAUNCH(13); break;
         case 9: RT_LAUNCH(9); break;
         default: RT_LAUNCH(0);
     }
