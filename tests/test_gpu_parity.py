@@ -448,6 +448,30 @@ def test_full_size_snort_1gib_kernels_agree():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.slow
+def test_full_size_merged_4gib_kernels_agree():
+    """BASELINE config 5 size (snort + et merged, 4 GiB: four 1 GiB launches
+    of the RT kernel): the two independent kernels agree at every position."""
+    torch = _torch()
+    rt, ac = matcher("merged", "rt"), matcher("merged", "ac")
+    n = 4 << 30
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    pm.load().pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 5, 0, s)
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = torch.empty(n, dtype=torch.int32, device="cuda")
+    ca = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cb = torch.zeros(1, dtype=torch.int64, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), ca.data_ptr(), s)
+    ac.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), cb.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert int(ca.item()) == int(cb.item())
+    assert int(ca.item()) > 0.95 * n  # merged: ~99 % of ASCII positions match something
+    del a, b, dt
+    torch.cuda.empty_cache()
+
+
 def test_adversarial_stream_large_rt_equals_ac():
     """A 32 MiB tiling of the shipped adversarial stream queues far more
     positions than the worklist holds, so the scan kernel's in-kernel
