@@ -527,6 +527,24 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             const uint32_t base = incl - c;
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
             if (V == 13) asm volatile("" ::"v"(base), "s"(total));  // ablation: scan only
+            if (V != 13 && total <= RT_QCAP - qn - rr.keep) {
+                // common case: the whole chunk fits; straight-line per-item
+                // body (the window's bytes i-3..i by one 64-bit shift)
+                uint32_t mm = cm, slot = qh + qn + base;
+                const uint32_t pbase = (uint32_t)(pc - pos0) + 4 * lane;
+                while (mm) {
+                    const uint32_t j = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    const uint32_t sg = j >> 2, b = j & 3;
+                    const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
+                    const u32x2 w = (sg & 2) ? w23 : w01;
+                    const uint32_t sl = slot & (RT_QCAP - 1);
+                    qkey[sl] = (uint32_t)((((uint64_t)w.y << 32) | w.x) >> (8 * (1 + b)));
+                    qpos[sl] = pbase + 256 * sg + b;
+                    ++slot;
+                }
+                qn += total;
+            } else
             for (uint32_t done = 0; V != 13;) {  // wave-uniform
                 // the in-flight round's possible survivors keep their room
                 const uint32_t room = RT_QCAP - qn - rr.keep;
