@@ -38,7 +38,7 @@ constexpr int RT_FILTER_WORDS = 4096;  // must match pm_flatten.h
 constexpr int RT_F3_WORDS = 256;        // stage-2 filter words, must match pm_flatten.h
 constexpr int RT_F2_WORDS = 2048;
 constexpr uint32_t RT_QCAP = 64;        // queue ring per wave (power of two, <= 64: one item per lane)
-constexpr uint32_t RT_ROUND = 48;       // a round is issued once this many are queued
+constexpr uint32_t RT_ROUND = 40;       // a round is issued once this many are queued
 constexpr int RT_CHUNK = 1024;         // positions per wave iteration
 constexpr uint32_t CONT16 = 0x8000u;
 constexpr uint32_t CONT32 = 0x80000000u;
