@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pm_flatten.h"
@@ -47,7 +48,27 @@ thread_local char g_err[512] = "";
 
 enum Kind { KIND_RT = 1, KIND_AC = 2 };
 
-constexpr size_t STAGE_POSITIONS = (size_t)64 << 20;  // read_block piece
+// read_block pipeline blocks (positions): the upload, kernel and download of
+// block k overlap the host finishing block k-1.  Gid output
+// is downloaded straight into the caller's array (no host work per block);
+// pattern-id output is mapped on the host, so smaller blocks overlap more
+// of that mapping with the transfers.
+constexpr size_t PIPE_GID_POSITIONS = (size_t)16 << 20;
+constexpr size_t PIPE_ID_POSITIONS = (size_t)8 << 20;
+
+// One pipeline slot: pinned host and device staging for one block and its
+// own stream, so two blocks are in flight.
+struct PipeSlot {
+    uint8_t* d_stage = nullptr;
+    uint32_t* d_res = nullptr;
+    uint8_t* h_stage = nullptr;
+    uint32_t* h_res = nullptr;
+    size_t cap = 0;  // positions
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool busy = false;
+    size_t off = 0, m = 0;  // block = positions [off, off + m) of the call
+};
 
 struct PmHip {
     int kind_req = KIND_RT;
@@ -69,15 +90,10 @@ struct PmHip {
     bool cache_hit = false;
     std::vector<void*> allocs;
     size_t table_bytes = 0;
-    // streaming
+    // streaming: the carried history and a two-slot pipeline (scan_host)
     std::vector<uint8_t> hist;
-    uint8_t* d_stage = nullptr;
-    uint32_t* d_res = nullptr;
-    uint8_t* h_stage = nullptr;
-    uint32_t* h_res = nullptr;
-    size_t stage_cap = 0;  // positions
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<pm_pattern_id_t> id_of_gid;  // [0] = PM_NULL_PATTERN_ID
+    PipeSlot slot[2];
     double dev_seconds = 0.0;
 };
 
@@ -105,21 +121,63 @@ PmHip* create(int kind) {
     return o;
 }
 
-void ensure_stage(PmHip* o, size_t positions) {
-    if (positions <= o->stage_cap) return;
-    if (o->d_stage) {
-        PM_CHECK(hipFree(o->d_stage));
-        PM_CHECK(hipFree(o->d_res));
-        PM_CHECK(hipHostFree(o->h_stage));
-        PM_CHECK(hipHostFree(o->h_res));
+void free_slot(PipeSlot& q) {
+    if (q.d_stage) {
+        (void)hipFree(q.d_stage);
+        (void)hipFree(q.d_res);
+        (void)hipHostFree(q.h_stage);
+        (void)hipHostFree(q.h_res);
     }
-    size_t cap = std::max(positions, (size_t)1 << 16);
-    size_t stage_bytes = cap + o->max_len + 64;
-    PM_CHECK(hipMalloc(&o->d_stage, stage_bytes));
-    PM_CHECK(hipMalloc(&o->d_res, cap * sizeof(uint32_t)));
-    PM_CHECK(hipHostMalloc(&o->h_stage, stage_bytes, hipHostMallocDefault));
-    PM_CHECK(hipHostMalloc(&o->h_res, cap * sizeof(uint32_t), hipHostMallocDefault));
-    o->stage_cap = cap;
+    q.d_stage = nullptr;
+    q.cap = 0;
+}
+
+void ensure_slot(PmHip* o, PipeSlot& q, size_t positions) {
+    if (!q.stream) {
+        PM_CHECK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+        PM_CHECK(hipEventCreate(&q.ev0));
+        PM_CHECK(hipEventCreate(&q.ev1));
+    }
+    if (positions <= q.cap) return;
+    free_slot(q);
+    const size_t cap = std::max(positions, (size_t)1 << 16);
+    const size_t stage_bytes = cap + o->max_len + 64;
+    PM_CHECK(hipMalloc(&q.d_stage, stage_bytes));
+    PM_CHECK(hipMalloc(&q.d_res, cap * sizeof(uint32_t)));
+    PM_CHECK(hipHostMalloc(&q.h_stage, stage_bytes, hipHostMallocDefault));
+    PM_CHECK(hipHostMalloc(&q.h_res, cap * sizeof(uint32_t), hipHostMallocDefault));
+    q.cap = cap;
+}
+
+// Host threads for the copy/map work around the pipeline (PM_HOST_THREADS,
+// default min(8, hardware threads)).
+unsigned host_threads() {
+    static const unsigned t = [] {
+        const char* e = std::getenv("PM_HOST_THREADS");
+        long v = e ? std::strtol(e, nullptr, 10) : 0;
+        if (v <= 0) v = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        return (unsigned)std::min(v, 64L);
+    }();
+    return t;
+}
+
+// f(lo, hi) over [0, n) split across host threads, pieces of at least grain.
+template <class F>
+void par_range(size_t n, size_t grain, const F& f) {
+    const size_t parts = std::min<size_t>(host_threads(), std::max<size_t>(1, n / grain));
+    if (parts <= 1) {
+        f((size_t)0, n);
+        return;
+    }
+    const size_t step = (n + parts - 1) / parts;
+    std::vector<std::thread> th;
+    th.reserve(parts - 1);
+    for (size_t k = 1; k < parts; ++k) {
+        const size_t lo = std::min(n, k * step), hi = std::min(n, lo + step);
+        th.emplace_back([&f, lo, hi] { f(lo, hi); });
+    }
+    f((size_t)0, std::min(n, step));
+    for (auto& t : th) t.join();
 }
 
 hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
@@ -128,43 +186,83 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
     return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
 }
 
-// Scan n new bytes after the carried history; gids to out_gid.
-void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid) {
+// Scan n new bytes after the carried history.  Results go to out_gid (gids)
+// or out_ids (the caller's pattern ids, PM_NULL_PATTERN_ID for none) -- one
+// of the two is non-null.  Blocks alternate between two slots (streams):
+// block k's bytes are uploaded straight from the caller's buffer behind its
+// context -- the last max_len-1 stream bytes before it (carried history,
+// then the caller's own buffer), staged in pinned memory -- scanned, and the
+// gids downloaded straight into out_gid, or into pinned memory from which
+// the host maps them to pattern ids (threads) while block k+1 is in flight.
+// Measured rates: DESIGN.md §5.
+void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pattern_id_t* out_ids) {
     if (!o->compiled) {
         std::fprintf(stderr, "pm_hip: read before compile\n");
         std::exit(EXIT_FAILURE);
     }
     PM_CHECK(hipSetDevice(o->device));
     const size_t keep = o->max_len ? o->max_len - 1 : 0;
-    size_t done = 0;
-    while (done < n) {
-        const size_t m = std::min(STAGE_POSITIONS, n - done);
-        ensure_stage(o, m);
-        const size_t h = o->hist.size();
-        const size_t ctx = (h + 15) & ~(size_t)15;  // new bytes start 16-aligned
-        std::memcpy(o->h_stage + ctx - h, o->hist.data(), h);
-        std::memcpy(o->h_stage + ctx, buf + done, m);
-        std::memset(o->h_stage + ctx + m, 0, 16);
-        PM_CHECK(hipMemcpyAsync(o->d_stage, o->h_stage, ctx + m + 16, hipMemcpyHostToDevice, o->stream));
-        PM_CHECK(hipEventRecord(o->ev0, o->stream));
-        PM_CHECK(launch(o, o->d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, o->d_res, 4, nullptr, o->stream));
-        PM_CHECK(hipEventRecord(o->ev1, o->stream));
-        PM_CHECK(hipMemcpyAsync(o->h_res, o->d_res, m * sizeof(uint32_t), hipMemcpyDeviceToHost, o->stream));
-        PM_CHECK(hipStreamSynchronize(o->stream));
+    const size_t pipe = out_gid ? PIPE_GID_POSITIONS : PIPE_ID_POSITIONS;
+    auto finish = [&](PipeSlot& q) {
+        PM_CHECK(hipStreamSynchronize(q.stream));
         float ms = 0.f;
-        PM_CHECK(hipEventElapsedTime(&ms, o->ev0, o->ev1));
+        PM_CHECK(hipEventElapsedTime(&ms, q.ev0, q.ev1));
         o->dev_seconds += ms * 1e-3;
-        std::memcpy(out_gid + done, o->h_res, m * sizeof(uint32_t));
-        // carry the last `keep` bytes of the stream
-        if (keep) {
-            if (m >= keep) {
-                o->hist.assign(buf + done + m - keep, buf + done + m);
-            } else {
-                o->hist.insert(o->hist.end(), buf + done, buf + done + m);
-                if (o->hist.size() > keep) o->hist.erase(o->hist.begin(), o->hist.end() - keep);
-            }
+        if (!out_gid) {
+            const uint32_t* g = q.h_res;
+            pm_pattern_id_t* dst = out_ids + q.off;
+            const pm_pattern_id_t* map = o->id_of_gid.data();
+            par_range(q.m, (size_t)1 << 18, [&](size_t lo, size_t hi) {
+                for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
+            });
         }
+        q.busy = false;
+    };
+    size_t done = 0;
+    for (int k = 0; done < n; ++k) {
+        PipeSlot& q = o->slot[k & 1];
+        if (q.busy) finish(q);
+        const size_t m = std::min(pipe, n - done);
+        ensure_slot(o, q, m);
+        // context: the last `keep` bytes of (history | buf[0, done))
+        const size_t h = std::min(keep, o->hist.size() + done);
+        const size_t ctx = (h + 15) & ~(size_t)15;  // new bytes start 16-aligned
+        uint8_t* st = q.h_stage + ctx - h;
+        if (done >= h) {
+            std::memcpy(st, buf + done - h, h);
+        } else {
+            const size_t from_hist = h - done;
+            std::memcpy(st, o->hist.data() + o->hist.size() - from_hist, from_hist);
+            std::memcpy(st + from_hist, buf, done);
+        }
+        std::memset(q.h_stage + ctx, 0, 16);
+        if (ctx) PM_CHECK(hipMemcpyAsync(q.d_stage, q.h_stage, ctx, hipMemcpyHostToDevice, q.stream));
+        PM_CHECK(hipMemcpyAsync(q.d_stage + ctx, buf + done, m, hipMemcpyHostToDevice, q.stream));
+        PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
+        PM_CHECK(hipEventRecord(q.ev0, q.stream));
+        PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, 4, nullptr, q.stream));
+        PM_CHECK(hipEventRecord(q.ev1, q.stream));
+        PM_CHECK(hipMemcpyAsync(out_gid ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, q.stream));
+        q.busy = true;
+        q.off = done;
+        q.m = m;
         done += m;
+    }
+    // oldest block first
+    for (int k = 0; k < 2; ++k) {
+        PipeSlot& a = o->slot[0], &b = o->slot[1];
+        PipeSlot& q = (a.busy && (!b.busy || a.off < b.off)) ? a : b;
+        if (q.busy) finish(q);
+    }
+    // carry the last `keep` bytes of the stream
+    if (keep && n) {
+        if (n >= keep) {
+            o->hist.assign(buf + n - keep, buf + n);
+        } else {
+            o->hist.insert(o->hist.end(), buf, buf + n);
+            if (o->hist.size() > keep) o->hist.erase(o->hist.begin(), o->hist.end() - keep);
+        }
     }
 }
 
@@ -231,28 +329,18 @@ void pm_hip_compile(void* obj) {
     o->d_parent = (const uint32_t*)dalloc_copy(o, im.par.parent.data(), im.par.parent.size() * 4);
     o->d_depth = (const uint32_t*)dalloc_copy(o, im.par.depth.data(), im.par.depth.size() * 4);
     o->parent = std::move(im.par.parent);
-    PM_CHECK(hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking));
-    PM_CHECK(hipEventCreate(&o->ev0));
-    PM_CHECK(hipEventCreate(&o->ev1));
+    o->id_of_gid.assign(o->gids.index_of_gid.size(), PM_NULL_PATTERN_ID);
+    for (size_t g = 1; g < o->gids.index_of_gid.size(); ++g) o->id_of_gid[g] = o->ids[o->gids.index_of_gid[g]];
     o->compiled = true;
 }
 
 int pm_hip_read_block_gid(void* obj, const uint8_t* buf, size_t n, uint32_t* out_gid) {
-    scan_host(as(obj), buf, n, out_gid);
+    scan_host(as(obj), buf, n, out_gid, nullptr);
     return 0;
 }
 
 void pm_hip_read_block(void* obj, const char* buf, size_t n, pm_pattern_id_t* out) {
-    PmHip* o = as(obj);
-    std::vector<uint32_t> g(std::min(n, STAGE_POSITIONS));
-    size_t done = 0;
-    while (done < n) {
-        size_t m = std::min(n - done, g.size());
-        scan_host(o, reinterpret_cast<const uint8_t*>(buf) + done, m, g.data());
-        for (size_t j = 0; j < m; ++j)
-            out[done + j] = g[j] ? o->ids[o->gids.index_of_gid[g[j]]] : PM_NULL_PATTERN_ID;
-        done += m;
-    }
+    scan_host(as(obj), reinterpret_cast<const uint8_t*>(buf), n, nullptr, out);
 }
 
 // The per-byte entry point of the reference ABI.  It runs the same GPU scan
@@ -279,15 +367,12 @@ void pm_hip_free(void* obj) {
     PmHip* o = as(obj);
     (void)hipSetDevice(o->device);
     for (void* p : o->allocs) (void)hipFree(p);
-    if (o->d_stage) {
-        (void)hipFree(o->d_stage);
-        (void)hipFree(o->d_res);
-        (void)hipHostFree(o->h_stage);
-        (void)hipHostFree(o->h_res);
+    for (PipeSlot& q : o->slot) {
+        free_slot(q);
+        if (q.ev0) (void)hipEventDestroy(q.ev0);
+        if (q.ev1) (void)hipEventDestroy(q.ev1);
+        if (q.stream) (void)hipStreamDestroy(q.stream);
     }
-    if (o->ev0) (void)hipEventDestroy(o->ev0);
-    if (o->ev1) (void)hipEventDestroy(o->ev1);
-    if (o->stream) (void)hipStreamDestroy(o->stream);
     delete o;
 }
 

@@ -137,6 +137,15 @@ class HipMatcher:
         self.lib.pm_hip_read_block(self.obj, data, n, out)
         return [x or 0 for x in out[:n]]
 
+    def read_block_id_array(self, data) -> np.ndarray:
+        """pm_hip_read_block into a numpy uintp array (pattern id per position)."""
+        arr = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray)
+                                   else data, dtype=np.uint8)
+        out = np.empty(max(len(arr), 1), dtype=np.uintp)
+        self.lib.pm_hip_read_block(self.obj, arr.ctypes.data_as(ctypes.c_char_p), len(arr),
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p)))
+        return out[:len(arr)]
+
     def total_mem(self):
         return self.lib.pm_hip_total_mem(self.obj)
 

@@ -77,6 +77,39 @@ def test_state_carries_across_read_block_calls(kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
+def test_read_block_pipeline_blocks(kind):
+    """The host path pipelines 8 Mi-position blocks over two slots
+    (pm_plugin.hip scan_host): a 20 MiB stream read in one call, and in calls
+    cut around the block edges, equals one device-resident scan of it; the
+    pattern-id form is the gid's add_pattern id."""
+    import ctypes
+    torch = _torch()
+    m = matcher("merged", kind)
+    n = (20 << 20) + 12345
+    text = pm.gen_stream(n, 5, 0)
+    dev = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    m.scan_device(dev.data_ptr(), 0, 0, n, out.data_ptr(), cnt.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    exp = out.cpu().numpy().view(np.uint32)
+    m.reset()
+    assert np.array_equal(m.read_block_gids(text), exp)
+    B = 8 << 20
+    cuts = [0, 1, 7, B - 3, B + 5, 2 * B, 2 * B + 1, 2 * B + 100000, n - 2, n]
+    m.reset()
+    parts = [m.read_block_gids(text[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    assert np.array_equal(np.concatenate(parts), exp)
+    d = m._dict
+    size = ctypes.sizeof(pm._lib.PmPattern)
+    P = m.lib.pm_hip_n_patterns(m.obj)
+    pid = m.gid_codes(np.uint64(d.pattern_ptr(0)) + np.arange(P, dtype=np.uint64) * np.uint64(size))
+    m.reset()
+    ids = m.read_block_id_array(text)
+    assert np.array_equal(ids.astype(np.uint64), pid[exp])
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_read_char_per_byte(kind):
     m = matcher("merged", kind)
     o = oracle_for("merged")
