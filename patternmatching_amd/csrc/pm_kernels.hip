@@ -190,15 +190,22 @@ __device__ __forceinline__ void put_id(void* out, int64_t k, uint32_t v) {
     if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[k] = (uint16_t)v;
 }
 
-template <int V, int OUTW>
+template <int VT, int OUTW>
 __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
                                                              int64_t pos0, int64_t n, void* __restrict__ out,
                                                              unsigned long long* __restrict__ count, RtDev t) {
-    __shared__ __attribute__((aligned(16))) uint16_t s_t[RT_T2_U16];
-    __shared__ __attribute__((aligned(16))) uint32_t s_f[RT_FILTER_WORDS];
-    __shared__ __attribute__((aligned(16))) uint32_t s_f2[RT_F2_WORDS];
-    __shared__ uint32_t s_qkey[RT_WAVES][RT_QCAP];  // 128 + 16 + 8 + 8 KiB: all of the CU's LDS
-    __shared__ uint32_t s_qpos[RT_WAVES][RT_QCAP];
+    // One LDS block with fixed offsets, 16 + 128 + 8 + 8 KiB: all of the
+    // CU's LDS.  The stage-1 filter sits at address 0, so a filter word's
+    // address is the hash bits alone, and t12 at 16 KiB, which fits the
+    // ds_read offset field: neither per-position address needs a base add.
+    __shared__ __attribute__((aligned(16)))
+    uint32_t s_lds[RT_FILTER_WORDS + RT_T2_U16 / 2 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP];
+    uint32_t* const s_f = s_lds;
+    uint16_t* const s_t = reinterpret_cast<uint16_t*>(s_lds + RT_FILTER_WORDS);
+    uint32_t* const s_f2 = s_lds + RT_FILTER_WORDS + RT_T2_U16 / 2;
+    uint32_t(*const s_qkey)[RT_QCAP] =
+        reinterpret_cast<uint32_t(*)[RT_QCAP]>(s_lds + RT_FILTER_WORDS + RT_T2_U16 / 2 + RT_F2_WORDS);
+    uint32_t(*const s_qpos)[RT_QCAP] = s_qkey + RT_WAVES;
     {
         const uint4* src = reinterpret_cast<const uint4*>(t.t12);
         uint4* dst = reinterpret_cast<uint4*>(s_t);
@@ -211,6 +218,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     }
     __syncthreads();
 
+    // VT >= 20: variant VT - 20 with each wave on a contiguous span of chunks
+    constexpr int V = VT >= 20 ? VT - 20 : VT;
+    constexpr bool kSpan = VT >= 20;
     // ablation phase switches (V = 0: all on)
     constexpr bool kFilter = V == 0 || V >= 5;
     constexpr bool kPush = kFilter && V != 11;
@@ -221,7 +231,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t* qkey = s_qkey[wid];
     uint32_t* qpos = s_qpos[wid];
-    uint32_t cnt = 0;
+    uint32_t cnt = 0;   // per lane
+    uint32_t scnt = 0;  // per wave (scalar): the chunks' nonzero placeholders
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tA = 0, tB = 0;
     if (V == 9) tA = stamp();
@@ -230,7 +241,20 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
     const int64_t c_hi = n / RT_CHUNK;
     const int64_t c_lo = pos0 - stream_start >= 2 ? 0 : 1;
-    const int64_t stride = (int64_t)gridDim.x * RT_WAVES;
+    // this wave's chunks: cbeg, cbeg + cstep, ... below cend
+    const int64_t gw = (int64_t)blockIdx.x * RT_WAVES + wid;
+    const int64_t nw = (int64_t)gridDim.x * RT_WAVES;
+    int64_t cbeg, cend, cstep;
+    if (kSpan) {
+        const int64_t per = (c_hi - c_lo + nw - 1) / nw;
+        cbeg = c_lo + gw * per;
+        cend = cbeg + per < c_hi ? cbeg + per : c_hi;
+        cstep = 1;
+    } else {
+        cbeg = c_lo + gw;
+        cend = c_hi;
+        cstep = nw;
+    }
     // out-of-range prefetches read this instead (any >= 1 KiB of table)
     const uint8_t* dummy = reinterpret_cast<const uint8_t*>(t.filt) + 4;
     using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
@@ -406,7 +430,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // that all lanes load (one line); the three look-back bytes of a lane
     // come from its neighbour by DPP (chunk()).
     auto fetch = [&](uint32_t (&xr)[4], uint32_t& xp, int64_t c) __attribute__((always_inline)) {
-        const uint8_t* base = c < c_hi ? text + pos0 + c * RT_CHUNK : dummy;
+        const uint8_t* base = c < cend ? text + pos0 + c * RT_CHUNK : dummy;
 #pragma unroll
         for (int s = 0; s < 4; ++s)
             xr[s] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(base + 256 * s + 4 * lane));
@@ -428,7 +452,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     rr.n = 0;
     rr.keep = 0;
     uint32_t xa[4], xb[4], pa, pb;
-    int64_t ch = c_lo + (int64_t)blockIdx.x * RT_WAVES + wid;
+    int64_t ch = cbeg;
     // One chunk: depth<=2 answers from LDS, filter, the previous chunk's
     // round consumed and a new one issued, the store,
     // the push of this chunk's candidates, the prefetch two chunks ahead.
@@ -476,13 +500,13 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         }
 #undef RT_KEY
 #undef RT_RAW
-        uint32_t nzm = 0;  // bit j: placeholder j is nonzero
+        // nonzero placeholders, counted on the scalar unit: one compare per
+        // position into a lane mask, then s_bcnt1
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             res[j] &= 0x7FFFu;
-            nzm |= (uint32_t)(res[j] != 0u) << j;
+            scnt += (uint32_t)__popcll(__ballot(res[j] != 0u));
         }
-        cnt += __popc(nzm);
         if (V == 9) { const uint64_t u = stamp(); ph[0] += u - tB; tB = u; }
         if (V == 11) asm volatile("" ::"v"(cm));  // keeps the filter live
         if (kRounds) {
@@ -585,7 +609,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 qn = 0;
             }
         }
-        fetch(xr, xp, c + 2 * stride);
+        fetch(xr, xp, c + 2 * cstep);
     };
     // Enter the loop with the memory-op pattern of the steady state (round,
     // store, prefetch; round, store, prefetch) so the compiler's vmcnt is the
@@ -596,13 +620,13 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     fetch(xa, pa, ch);
     if (kRounds) issue(rr, 0);
     stand_in_store();
-    fetch(xb, pb, ch + stride);
+    fetch(xb, pb, ch + cstep);
     for (;;) {  // wave-uniform
-        if (ch >= c_hi) break;
+        if (ch >= cend) break;
         chunk(xa, pa, ch);
-        if (ch + stride >= c_hi) break;
-        chunk(xb, pb, ch + stride);
-        ch += 2 * stride;
+        if (ch + cstep >= cend) break;
+        chunk(xb, pb, ch + cstep);
+        ch += 2 * cstep;
     }
     if (kRounds) {
         if (rr.n) consume(rr);
@@ -642,6 +666,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     }
     if (count) {
         for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o);
+        cnt += scnt;
         if (lane == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
     }
 }
@@ -837,6 +862,8 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 12: RT_LAUNCH(12); break;
         case 13: RT_LAUNCH(13); break;
         case 9: RT_LAUNCH(9); break;
+        case 20: RT_LAUNCH(20); break;
+        case 22: RT_LAUNCH(22); break;
         default: RT_LAUNCH(0);
     }
 #undef RT_LAUNCH
