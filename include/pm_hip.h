@@ -143,6 +143,9 @@ int pm_hip_set_device(int device);
  * the default grid.  Outputs of variants 1-2 are not match ids. */
 int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out,
                               int out_width, unsigned long long* d_count, void* hip_stream, int blocks);
+/* Launch shape of the AC-DFA kernel for timing sweeps: segments in flight
+ * (lanes) per CU; 0 restores the default. */
+void pm_hip_debug_dfa_shape(int lanes_per_cu);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

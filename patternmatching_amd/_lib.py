@@ -105,6 +105,7 @@ SIGNATURES = {
     "pm_hip_set_device": (ctypes.c_int, [ctypes.c_int]),
     "pm_hip_debug_scan_variant": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int64, c_vp, ctypes.c_int,
                                                  c_vp, c_vp, ctypes.c_int]),
+    "pm_hip_debug_dfa_shape": (None, [ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
     "pm_flat_build_cached": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int,
@@ -139,6 +140,8 @@ def load():
                            "(or __graft_entry__.build()); there is no CPU fallback")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if name.startswith("pm_hip_debug_") and not hasattr(lib, name):
+            continue  # timing hooks: older builds under A/B comparison may lack one
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

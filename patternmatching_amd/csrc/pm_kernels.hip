@@ -881,14 +881,20 @@ hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream
     return launch_rt_impl(variant, text, stream_start, pos0, n, out, outw, count, t, num_cu, s, blocks_override);
 }
 
+// DFA launch shape: lanes (segments in flight) per CU; pm_dfa_set_shape
+// sweeps it.  More lanes than this measured slower: the gathers then touch
+// more distinct table lines than the caches hold.
+constexpr int DFA_LANES_PER_CU = 512;
+static int g_dfa_lanes_per_cu = DFA_LANES_PER_CU;
+
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (!out) outw = 0;
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
-    // enough segments for ~8 waves per CU, each at least 2 KiB so the
-    // max_len-1 warm-up stays a small fraction
-    const int64_t lanes = (int64_t)num_cu * 512;
+    // one segment per lane, each at least 2 KiB so the max_len-1 warm-up
+    // stays a small fraction
+    const int64_t lanes = (int64_t)num_cu * g_dfa_lanes_per_cu;
     int64_t seg = (n + lanes - 1) / lanes;
     if (seg < 2048) seg = 2048;
     seg = (seg + 15) & ~(int64_t)15;
@@ -904,6 +910,8 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         hipLaunchKernelGGL(dfa_scan_kernel<0>, g, b, 0, s, text, stream_start, pos0, n, out, count, t, seg);
     return hipGetLastError();
 }
+
+void pm_dfa_set_shape(int lanes_per_cu) { g_dfa_lanes_per_cu = lanes_per_cu > 0 ? lanes_per_cu : DFA_LANES_PER_CU; }
 
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,
                           const uint32_t* depth, unsigned long long* counts, int num_cu, hipStream_t s) {

@@ -481,6 +481,8 @@ int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int
     return e == hipSuccess ? 0 : -3;
 }
 
+void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }
+
 int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
                              void* hip_stream) {
     hipError_t e = pm_launch_gen(d_dst, offset, n, seed, mode, (hipStream_t)hip_stream);
