@@ -642,25 +642,20 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             for (int k = 0; k < 8; ++k) atomicAdd(count + k, (unsigned long long)ph[k]);
         return;
     }
-    // the (at most two) chunks that touch the stream start or the tail, one
-    // position at a time, by two waves of the last workgroup
-    if (blockIdx.x == gridDim.x - 1 && wid < 2) {
-        int64_t c = -1;
-        if (wid == 0 && c_lo == 1) c = 0;
-        if (wid == 1 && c_hi < nchunks && !(c_lo == 1 && c_hi == 0)) c = c_hi;
-        if (c >= 0) {
-            const int64_t pc = pos0 + c * RT_CHUNK;
+    // the (at most two) chunks that touch the stream start or the tail: one
+    // position per thread of the last workgroup (a chunk is 1024 positions),
+    // so each costs one walk's latency, not sixteen
+    if (blockIdx.x == gridDim.x - 1) {
 #pragma unroll 1
-            for (int s = 0; s < 4; ++s) {
-                const int64_t p = pc + 256 * s + 4 * lane;
-#pragma unroll 1
-                for (int b = 0; b < 4; ++b) {
-                    if (p + b < pos0 + n) {
-                        const uint32_t v = rt_one(text, s_t, t, p + b, stream_start);
-                        if (OUTW) put_id<OUTW>(out, p + b - pos0, v);
-                        cnt += v != 0u;
-                    }
-                }
+        for (int e = 0; e < 2; ++e) {  // uniform
+            int64_t c = -1;
+            if (e == 0 && c_lo == 1) c = 0;
+            if (e == 1 && c_hi < nchunks && !(c_lo == 1 && c_hi == 0)) c = c_hi;
+            const int64_t p = pos0 + c * RT_CHUNK + threadIdx.x;
+            if (c >= 0 && p < pos0 + n) {
+                const uint32_t v = rt_one(text, s_t, t, p, stream_start);
+                if (OUTW) put_id<OUTW>(out, p - pos0, v);
+                cnt += v != 0u;
             }
         }
     }
