@@ -42,7 +42,9 @@ def parse():
     p.add_argument("--mode", default="dense", choices=list(WIDTH),
                    help="dense: u32 id per position; dense16: u16 id per position; count: match count only")
     p.add_argument("--kernel", default="rt", choices=["rt", "ac"])
-    p.add_argument("--stream", default="ascii", choices=["ascii", "bytes"])
+    p.add_argument("--stream", default="ascii", choices=["ascii", "bytes", "ship"],
+                   help="ascii / bytes: seeded synthetic (DESIGN.md §5); ship: the reference's shipped "
+                        "dictionaries_generated.stream tiled to --bytes (adversarial: deep matches)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-sample", type=int, default=256 << 20, help="bytes of the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
@@ -126,7 +128,7 @@ def main():
 
     # CPU leg first, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.stream != "ship":
         cpu = cpu_baseline(args)
 
     import torch
@@ -151,8 +153,13 @@ def main():
     stream = torch.cuda.current_stream()
     text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     seed = args.seed + rank  # independent shard per rank
-    if lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, seed, 0 if args.stream == "ascii" else 1,
-                                    stream.cuda_stream) != 0:
+    if args.stream == "ship":
+        import numpy as np
+        ship = torch.from_numpy(np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8))
+        reps = (n + 64 + ship.numel() - 1) // ship.numel()
+        text.copy_(ship.to("cuda").repeat(reps)[: n + 64])
+    elif lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, seed, 0 if args.stream == "ascii" else 1,
+                                      stream.cuda_stream) != 0:
         raise RuntimeError(lib.pm_hip_last_error().decode())
     width = WIDTH[args.mode]
     out = torch.empty(n, dtype={4: torch.int32, 2: torch.int16}[width], device="cuda") if width else None
@@ -246,8 +253,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: seeded splitmix64 %s stream per GPU (DESIGN.md §5), generated in HBM; "
-                    "dictionaries from the reference" % args.stream,
+            "data": ("synthetic: seeded splitmix64 %s stream per GPU (DESIGN.md §5), generated in HBM; "
+                     "dictionaries from the reference" % args.stream) if args.stream != "ship" else
+                    "the reference's shipped Streams/dictionaries_generated.stream (10,240 B) tiled in HBM; "
+                    "dictionaries from the reference",
             "config": {
                 "workload": f"{args.dict}.dict, {n} B {args.stream} stream per GPU, "
                             + {"dense": "dense u32 match id per position", "dense16": "dense u16 match id per position",

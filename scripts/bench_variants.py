@@ -16,7 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--dict", default="snort")
 ap.add_argument("--bytes", type=int, default=1 << 30)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--stream", type=int, default=0)
+ap.add_argument("--stream", type=int, default=0, help="0 ascii, 1 bytes, 2 the shipped stream tiled")
 ap.add_argument("--variants", default="0,1,2")
 ap.add_argument("--blocks", default="0")
 ap.add_argument("--modes", default="dense,dense16,count")
@@ -32,7 +32,12 @@ m.compile()
 n = args.bytes
 s = torch.cuda.current_stream()
 text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, 1, args.stream, s.cuda_stream)
+if args.stream == 2:
+    import numpy as np
+    ship = torch.from_numpy(np.fromfile(os.path.join(data, "dictionaries_generated.stream"), dtype=np.uint8))
+    text.copy_(ship.cuda().repeat((n + 64) // ship.numel() + 1)[: n + 64])
+else:
+    lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, 1, args.stream, s.cuda_stream)
 out = torch.empty(n, dtype=torch.int32, device="cuda")
 cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
 variants = [(int(v), mode, int(b)) for v in args.variants.split(",") for mode in args.modes.split(",")
