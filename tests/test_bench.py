@@ -1,0 +1,86 @@
+"""bench.py keeps the driver's contract: one JSON line with the required
+keys, whole-job value = bytes / wall time, roofline from the kernel time,
+and the CPU baseline leg (the reference's loop; the C port without it)."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
+
+
+def _bench_args(**kw):
+    sys.path.insert(0, REPO)
+    import bench
+    a = dict(gpus=1, steps=1, warmup=0, dict="et", bytes=1 << 20, mode="dense", kernel="rt", stream="ascii", seed=1,
+             cpu_sample=1 << 20, no_cpu=False, score=False)
+    a.update(kw)
+    return bench, argparse.Namespace(**a)
+
+
+def test_cpu_baseline_leg_small_sample():
+    """The CPU leg runs without a GPU: the reference's loop on a 1 MiB
+    sample (one process per host core) or, without that binary, the port."""
+    bench, args = _bench_args()
+    cpu = bench.cpu_baseline(args)
+    assert cpu["unit"] == "GB/s" and cpu["value"] > 0 and cpu["cores"] >= 1
+    assert cpu["kind"] in ("reference", "port")
+    if cpu["kind"] == "reference":
+        assert cpu["single_core"]["nonnull"] > 0 and cpu["per_core_min"] > 0
+
+
+def _run(extra, env=None):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--bytes", str(16 << 20), "--steps", "2", "--warmup", "1",
+           "--no-cpu"] + extra
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=e, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_json_line_contract():
+    d = _run([])
+    for k in REQUIRED:
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["scaling"] == "weak" and d["unit"] == "GB/s" and d["dtype"] == "u8" and d["vs_baseline"] is None
+    assert "workload" in d["config"]
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    # achieved = 5 algorithmic B per position / kernel time; value = bytes / wall time
+    assert abs(r["achieved"] - (16 << 20) * 5 / (d["kernel_ms"] * 1e-3) / 1e9) / r["achieved"] < 0.01
+    assert abs(d["value"] - (16 << 20) / (d["ms_per_step"] * 1e-3) / 1e9) / d["value"] < 0.02
+    assert d["matches_per_step"] > 0.8 * (16 << 20)  # snort on ASCII: ~92 % non-null
+
+
+@pytest.mark.gpu
+def test_bench_rccl_path_at_world_one():
+    """PM_BENCH_DIST=1: the multi-GPU code (RCCL init, barriers, the max and
+    sum all-reduces) at world size 1 gives the same match count."""
+    plain = _run(["--mode", "count"])
+    env = {"PM_BENCH_DIST": "1", "RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
+           "MASTER_PORT": "29533", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    dist = _run(["--mode", "count"], env)
+    assert dist["matches_per_step"] == plain["matches_per_step"]
+    assert dist["n_gpus"] == 1
+
+
+@pytest.mark.gpu
+def test_bench_shipped_stream_and_score():
+    """--stream ship (deep matches everywhere) with --score: the RT ids equal
+    the AC instance's at every position."""
+    d = _run(["--stream", "ship", "--score", "--dict", "et"])
+    acc = d["accuracy"]
+    assert acc["success"] == acc["positions"] == 16 << 20
+    assert acc["false_pos_rate"] == acc["false_neg_rate"] == acc["partial_rate"] == 0.0
+    assert d["cpu_baseline"] is None
