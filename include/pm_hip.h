@@ -155,7 +155,7 @@ void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int
 void* pm_flat_build_cached(const char* const* pats, const uint32_t* lens, size_t n, int kind, const char* cache_dir);
 int pm_flat_cache_hit(void* handle);
 int pm_flat_fits(void* handle);
-/* name: "t12" "filt" "n2i" "t3" "rec" "next" "out" "index_of_gid"; returns element count */
+/* name: "t12" "filt" "t3h" "rec" "next" "out" "index_of_gid" "parent" "depth"; returns element count */
 size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* elem_size);
 void pm_flat_free(void* handle);
 

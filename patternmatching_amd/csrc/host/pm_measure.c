@@ -198,14 +198,12 @@ int pm_measure_all(PmConf* conf, PmDict* dict, PmInstanceStats* stats) {
         if (conf->verbose) { printf("Measuring algorithm %s...", e->name); fflush(stdout); }
         for (size_t f = 0; f < conf->n_stream_files; ++f) {
             int fd = open(conf->stream_files[f], O_RDONLY);
-            double dev0;
             if (fd == -1) {
                 fprintf(stderr, "can't open stream file %s: %s\n", conf->stream_files[f], strerror(errno));
                 exit(EXIT_FAILURE);
             }
             e->reset(inst[a].obj); /* measure.c:274-275 */
             if (reliable.obj != inst[a].obj) pm_mps_table[reliable.algo].reset(reliable.obj);
-            dev0 = 0.0;
             for (;;) {
                 size_t got = 0;
                 while (got < chunk) { /* fill the chunk (read() may return short) */
@@ -236,7 +234,6 @@ int pm_measure_all(PmConf* conf, PmDict* dict, PmInstanceStats* stats) {
                 }
                 if (got < chunk) break;
             }
-            (void)dev0;
             close(fd);
             st->device_seconds += pm_hip_device_seconds(inst[a].obj);
         }

@@ -364,6 +364,55 @@ bool load(const std::string& path, uint64_t key, int kind, PmImages& im) {
     return true;
 }
 
+// Values the kernels follow without bounds checks: table and record indices,
+// gids (score_kernel indexes parent[] with them) and the parent chain (which
+// score_kernel walks).  A file whose sizes validate but whose values do not
+// is rejected too, so a damaged cache can neither fault the device nor hang
+// a walk.
+bool values_ok(const PmImages& im, int kind, size_t ngid) {
+    if (ngid == 0 || im.par.parent.size() != ngid || im.par.depth.size() != ngid) return false;
+    const uint32_t P = (uint32_t)(ngid - 1);
+    const std::vector<uint32_t>& par = im.par.parent;
+    const std::vector<uint32_t>& dep = im.par.depth;
+    if (par[0] != 0 || dep[0] != 0) return false;
+    // depth[g] == 1 + depth[parent[g]] for every g admits no cycle
+    for (uint32_t g = 1; g <= P; ++g)
+        if (par[g] > P || dep[g] != 1 + dep[par[g]]) return false;
+    if (kind == 2) {
+        for (uint32_t x : im.dfa.next)
+            if (x >= im.dfa.states) return false;
+        for (uint32_t x : im.dfa.out)
+            if (x > P) return false;
+        return true;
+    }
+    const RtImage& rt = im.rt;
+    if (!rt.fits) return true;
+    if (rt.nrec >= (1u << 22)) return false;
+    for (uint16_t x : rt.t12)
+        if ((x & 0x7FFFu) > P) return false;
+    for (size_t e = 0; e < rt.t3h.size(); e += 4) {
+        const uint32_t x = rt.t3h[e], y = rt.t3h[e + 1], z = rt.t3h[e + 2], w = rt.t3h[e + 3];
+        if (!(x & RT_T3H_VALID)) continue;
+        const uint32_t k = x >> 25, nch = z >> 24, r = w & ~RT_CONT32;
+        if (y > P || k > 2) return false;
+        if (k == 1 && (nch < 1 || nch > RT_T3H_INLINE)) return false;
+        if (k == 1 && nch > 1 && (uint64_t)w + nch > rt.nrec) return false;
+        if (k == 1 && nch == 1 && ((w & RT_CONT32) ? r >= rt.nrec : w > P)) return false;
+        if (k == 2 && (!(w & RT_CONT32) || r >= rt.nrec)) return false;
+    }
+    for (uint32_t n = 0; n < rt.nrec; ++n) {
+        const uint32_t* R = &rt.rec[(size_t)n * RT_REC_WORDS];
+        if (R[9] > P) return false;
+        uint32_t pre = 0;
+        for (int w = 0; w < 8; ++w) {
+            if (((R[10 + (w >> 2)] >> (8 * (w & 3))) & 0xFFu) != pre) return false;
+            pre += (uint32_t)__builtin_popcount(R[w]);
+        }
+        if (pre && (uint64_t)R[8] + pre > rt.nrec) return false;
+    }
+    return true;
+}
+
 }  // namespace
 
 uint64_t pm_image_key(const std::vector<std::string>& pats, int kind) {
@@ -389,7 +438,7 @@ PmImages pm_build_images_cached(const std::vector<std::string>& pats, const PmGi
         char name[64];
         std::snprintf(name, sizeof name, "/pm-%d-%016llx.img", kind, (unsigned long long)key);
         path = dir + name;
-        if (load(path, key, kind, im) && im.par.parent.size() == g.index_of_gid.size()) {
+        if (load(path, key, kind, im) && values_ok(im, kind, g.index_of_gid.size())) {
             *hit = true;
             return im;
         }

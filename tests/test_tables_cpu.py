@@ -136,6 +136,14 @@ def test_compiled_image_cache(tmp_path):
         assert b.cache_hit
         for name in arrays:
             assert np.array_equal(a.array(name), b.array(name)), name
+        # sizes intact, one value damaged: parent[P] = P (a cycle) -> rejected, rebuilt
+        raw = bytearray(files[0].read_bytes())
+        ngid = len(a.array("parent"))
+        off = len(raw) - (16 + 4 * ngid) - 4
+        raw[off:off + 4] = (ngid - 1).to_bytes(4, "little")
+        files[0].write_bytes(bytes(raw))
+        assert not FlatImage(pats, kind, tmp_path).cache_hit
+        assert FlatImage(pats, kind, tmp_path).cache_hit
         # damage it: truncated, then garbage -> rebuilt and rewritten
         raw = files[0].read_bytes()
         files[0].write_bytes(raw[: len(raw) // 2])
