@@ -223,19 +223,6 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
     im.rec.assign((size_t)im.nrec * RT_REC_WORDS, 0);
     for (uint32_t v = first_d3; v < t.n; ++v) {
         uint32_t* R = &im.rec[(size_t)(v - first_d3) * RT_REC_WORDS];
-        if (t.ccount[v] == 1) {  // chain record (pm_flatten.h)
-            uint32_t u = v, len = 0;
-            do {
-                u = t.cstart[u];
-                const uint32_t b = 15 - len++;
-                R[b >> 2] |= (uint32_t)t.label[u] << (8 * (b & 3));
-            } while (len < RT_CHAIN_MAX && t.ccount[u] == 1 && !t.gid[u]);
-            R[8] = u - first_d3;
-            R[9] = best[v];
-            R[10] = len;
-            R[11] = RT_CHAIN;
-            continue;
-        }
         for (uint32_t k = 0; k < t.ccount[v]; ++k) {
             uint32_t c = t.label[t.cstart[v] + k];
             R[c >> 5] |= 1u << (c & 31);
@@ -301,7 +288,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 4;                     // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 3;                     // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);
@@ -416,10 +403,6 @@ bool values_ok(const PmImages& im, int kind, size_t ngid) {
     for (uint32_t n = 0; n < rt.nrec; ++n) {
         const uint32_t* R = &rt.rec[(size_t)n * RT_REC_WORDS];
         if (R[9] > P) return false;
-        if (R[11] == RT_CHAIN) {
-            if (R[10] < 1 || R[10] > RT_CHAIN_MAX || R[8] >= rt.nrec) return false;
-            continue;
-        }
         uint32_t pre = 0;
         for (int w = 0; w < 8; ++w) {
             if (((R[10 + (w >> 2)] >> (8 * (w & 3))) & 0xFFu) != pre) return false;

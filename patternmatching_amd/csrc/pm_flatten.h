@@ -39,8 +39,7 @@
 //                                           kind 2: RT_CONT32 | n3's record
 //             rec   u32[nrec * 12]    48-B records for nodes of depth >= 3:
 //                                     child bitmap[8], child base, best, 8 u8
-//                                     prefix popcounts; a node with one
-//                                     child: a chain record (RT_CHAIN)
+//                                     prefix popcounts
 //  DfaImage the Aho-Corasick automaton of Core/src/mpac.c (goto + BFS
 //           failure links + suffix/output links, :147-210) flattened into a
 //           dense DFA: next[s*256 + c] and out[s] (gid of the longest pattern
@@ -145,15 +144,3 @@ constexpr uint32_t RT_T3H_VALID = 1u << 24;
 inline uint32_t pm_rt_slot1(uint32_t k, uint32_t bits) { return pm_rt_hash(k) >> (32 - bits); }
 inline uint32_t pm_rt_slot2(uint32_t k, uint32_t bits) { return (k * 0x85EBCA77u) >> (32 - bits); }
 constexpr uint32_t RT_T3H_INLINE = 3;  // child bytes held in a t3h entry
-// Chain records: a node of depth >= 3 with exactly one child holds the unary
-// path below it, up to RT_CHAIN_MAX edges, ending after a pattern node or at
-// a node without exactly one child (so every node inside the path has the
-// record's best).  R[0..3]: the path bytes as a 16-B field in text order,
-// the j-th edge's byte at field byte 15 - j (a walk at depth d matches it
-// against text[i-d-j]); R[8] = the record of the path's last node; R[9] =
-// best; R[10] = the length; R[11] = RT_CHAIN.  A bitmap record's R[11] holds
-// the prefix counts of words 4..7, whose low byte is at most 128, so it is
-// never RT_CHAIN.  A walk through a long pattern takes ceil(len / 12) record
-// steps instead of len.
-constexpr uint32_t RT_CHAIN = 0xFFFFFFFFu;
-constexpr uint32_t RT_CHAIN_MAX = 12;

@@ -43,7 +43,6 @@ constexpr int RT_CHUNK = 1024;         // positions per wave iteration
 constexpr uint32_t CONT16 = 0x8000u;
 constexpr uint32_t CONT32 = 0x80000000u;
 constexpr uint32_t T3H_VALID = 1u << 24;
-constexpr uint32_t RT_CHAIN = 0xFFFFFFFFu;  // chain record marker in R[11], must match pm_flatten.h
 constexpr uint32_t RT_POSMASK = (1u << 30) - 1;  // queue item: position - pos0
 constexpr uint32_t RT_SLOT2 = 1u << 30;          // queue item: probe t3h slot2
 
@@ -116,18 +115,8 @@ __device__ __forceinline__ uint32_t rt_deep(const uint8_t* __restrict__ text, co
                                             uint32_t node, int64_t i, int64_t avail, int64_t d) {
     for (;;) {
         const uint32_t* R = rec + (size_t)node * 12;
-        const uint4 meta = *reinterpret_cast<const uint4*>(R + 8);  // {base, best, prefix} / {end, best, len, RT_CHAIN}
+        const uint4 meta = *reinterpret_cast<const uint4*>(R + 8);  // {base, best, prefix}
         if (d >= avail) return meta.y;
-        if (meta.w == RT_CHAIN) {  // the whole unary path, or the answer so far
-            if ((int64_t)meta.z > avail - d) return meta.y;
-            for (uint32_t j = 0; j < meta.z; ++j) {
-                const uint32_t b = 15 - j;
-                if (text[i - d - j] != ((R[b >> 2] >> (8 * (b & 3))) & 0xFFu)) return meta.y;
-            }
-            node = meta.x;
-            d += meta.z;
-            continue;
-        }
         const uint32_t c = text[i - d];
         const uint32_t w = c >> 5, bit = c & 31u;
         const uint32_t word = R[w];
@@ -140,34 +129,6 @@ __device__ __forceinline__ uint32_t rt_deep(const uint8_t* __restrict__ text, co
 
 __device__ __forceinline__ uint32_t rt_slot1(uint32_t k, uint32_t bits) { return rt_hash(k) >> (32 - bits); }
 __device__ __forceinline__ uint32_t rt_slot2(uint32_t k, uint32_t bits) { return (k * 0x85EBCA77u) >> (32 - bits); }
-
-// A record step loads a 16-B window of text around its byte text[q], q =
-// i - d: dword-aligned, ending with the dword that holds text[q] (so never
-// past i: d >= 3), starting no earlier than the stream's first dword.
-// text[q] is its byte q - rt_window(q), and so are the RT_CHAIN_MAX bytes
-// before it, or all of them back to the stream start.
-__device__ __forceinline__ int64_t rt_window(int64_t q, int64_t stream_start) {
-    const int64_t a = (q & ~(int64_t)3) - 12, lo = stream_start & ~(int64_t)3;
-    return a < lo ? lo : a;
-}
-// The len bytes of text ending at text[q] (byte o of window T) equal the
-// chain bytes of field F (text order, ending at byte 15).
-template <class V4>
-__device__ __forceinline__ bool rt_chain_match(const V4& T, uint32_t o, const V4& F, uint32_t len) {
-    uint64_t lo = T.x | (uint64_t)T.y << 32, hi = T.z | (uint64_t)T.w << 32;
-    const uint32_t sb = 8 * (15 - o);  // move text[q] to byte 15
-    if (sb >= 64) {
-        hi = lo << (sb - 64);
-        lo = 0;
-    } else if (sb) {
-        hi = (hi << sb) | (lo >> (64 - sb));
-        lo <<= sb;
-    }
-    const uint64_t flo = F.x | (uint64_t)F.y << 32, fhi = F.z | (uint64_t)F.w << 32;
-    const uint64_t mhi = len >= 8 ? ~0ull : ~0ull << (8 * (8 - len));
-    const uint64_t mlo = len > 8 ? ~0ull << (8 * (16 - len)) : 0ull;
-    return (((hi ^ fhi) & mhi) | ((lo ^ flo) & mlo)) == 0;
-}
 
 // The walk past depth 2 from key24 = text[i-2] | text[i-1] << 8 | text[i] << 16
 // (a depth-2 node with children) with c3 = text[i-3] when avail >= 4;
@@ -327,9 +288,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     struct Round {
         uint32_t n;     // items (wave-uniform)
         uint32_t keep;  // items that may survive the round (wave-uniform): ring room they hold
-        uint32_t fk, fp;
+        uint32_t fk, fp, tc;
         uint32_t skip;  // stage 2 rejected the item: its answer is the placeholder
-        u32x4 L0, L1, L2, T;  // T: a record step's text window (rt_window)
+        u32x4 L0, L1, L2;
     };
     // The queue is a ring of RT_QCAP items per wave: head qh, count qn.  A
     // round takes all queued items once RT_ROUND are queued
@@ -362,19 +323,15 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         const u32x4* a0 = deep ? R : (skip ? F : T + slot);
         const u32x4* a1 = deep ? R + 1 : F;
         const u32x4* a2 = deep ? R + 2 : F;
-        // (d < 3 only when a depth-512 walk wrapped d's 9 bits: a leaf, the
-        // window is not needed)
-        const uint32_t* a3 = (deep && d >= 3 && (int64_t)d <= i - stream_start)
-                                 ? reinterpret_cast<const uint32_t*>(text + rt_window(i - (int64_t)d, stream_start))
-                                 : reinterpret_cast<const uint32_t*>(F);
+        const uint8_t* a3 = (deep && (int64_t)d <= i - stream_start) ? text + (i - d) : dummy;
         if (V == 5) {  // ablation: every round load hits one line (results wrong)
             a0 = a1 = a2 = F;
-            a3 = reinterpret_cast<const uint32_t*>(F);
+            a3 = dummy;
         }
         r.L0 = *a0;
         r.L1 = *a1;
         r.L2 = *a2;
-        r.T = u32x4{a3[0], a3[1], a3[2], a3[3]};
+        r.tc = *a3;
         r.n = take;
         qh += take;
         qn -= take;
@@ -383,9 +340,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         // Nothing computed from the round may be hoisted above this point
         // (the compiler otherwise speculates it up to the loads and waits).
         // (Fenced copies: the round's own registers are never redefined.)
-        u32x4 L0 = r.L0, L1 = r.L1, L2 = r.L2, T = r.T;
-        uint32_t fk = r.fk, fp = r.fp;
-        asm volatile("" : "+v"(L0), "+v"(L1), "+v"(L2), "+v"(T), "+v"(fk), "+v"(fp)::"memory");
+        u32x4 L0 = r.L0, L1 = r.L1, L2 = r.L2;
+        uint32_t tc = r.tc, fk = r.fk, fp = r.fp;
+        asm volatile("" : "+v"(L0), "+v"(L1), "+v"(L2), "+v"(tc), "+v"(fk), "+v"(fp)::"memory");
         if (V == 9) { const uint64_t u = stamp(); ph[2] += u - tB; tB = u; }
         bool again = false;
         uint32_t nk = 0, np = 0;
@@ -427,19 +384,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 }
             } else {
                 d = fk >> 23;
-                v = L2.y;  // {base, best, prefix lo, prefix hi} or {end, best, length, RT_CHAIN}
-                const int64_t q = i - (int64_t)d;
-                const uint32_t o = (uint32_t)(q - rt_window(q, stream_start));  // text[q] is byte o of T
-                if ((int64_t)d < avail && L2.w == RT_CHAIN) {
-                    // the whole path (no pattern inside it) or the answer so far
-                    if ((int64_t)L2.z <= avail - (int64_t)d && rt_chain_match(T, o, L0, L2.z)) {
-                        node = L2.x;
-                        d += L2.z;
-                        again = true;
-                    }
-                } else if ((int64_t)d < avail) {
-                    const uint32_t tw = (o & 8) ? ((o & 4) ? T.w : T.z) : ((o & 4) ? T.y : T.x);
-                    const uint32_t tc = (tw >> (8 * (o & 3))) & 0xFFu;
+                v = L2.y;  // {base, best, prefix lo, prefix hi}
+                if ((int64_t)d < avail) {
                     const uint32_t w = tc >> 5, bit = tc & 31u;
                     // bit-test select tree (an equality chain becomes a
                     // dynamic extract, which lowers through scratch)

@@ -55,19 +55,6 @@ uint32_t rt_deep(const RtImage& im, const std::vector<uint8_t>& text, uint32_t n
         const size_t R = (size_t)node * RT_REC_WORDS;
         const uint32_t base = im.rec.at(R + 8), best = im.rec.at(R + 9);
         if (d >= avail) return best;
-        if (im.rec.at(R + 11) == RT_CHAIN) {  // the whole unary path, or the answer so far
-            const uint32_t len = im.rec.at(R + 10);
-            CHECK(len >= 1 && len <= RT_CHAIN_MAX, "chain length %u", len);
-            if ((int64_t)len > avail - d) return best;
-            for (uint32_t j = 0; j < len; ++j) {
-                const uint32_t b = 15 - j;
-                if (text.at(i - d - j) != ((im.rec.at(R + (b >> 2)) >> (8 * (b & 3))) & 0xFFu)) return best;
-            }
-            CHECK(base < im.nrec, "chain end %u of %u", base, im.nrec);
-            node = base;
-            d += len;
-            continue;
-        }
         const uint32_t c = text.at(i - d);
         const uint32_t w = c >> 5, bit = c & 31u;
         const uint32_t word = im.rec.at(R + w);
@@ -235,8 +222,7 @@ int main(int argc, char** argv) {
     const RtImage& im = rt2.rt;
     const DfaImage& dfa = df2.dfa;
     uint32_t s = 0;
-    size_t nonnull = 0, deep = 0, chains = 0;
-    for (uint32_t r = 0; r < im.nrec; ++r) chains += im.rec.at((size_t)r * RT_REC_WORDS + 11) == RT_CHAIN;
+    size_t nonnull = 0, deep = 0;
     for (int64_t i = 0; i < (int64_t)text.size(); ++i) {
         s = dfa.next.at((size_t)s * 256 + text[i]);
         CHECK(s < dfa.states, "state %u", s);
@@ -255,7 +241,7 @@ int main(int argc, char** argv) {
     }
     pm_dict_free(d);
     if (g_fail) return 1;
-    std::printf("ok patterns=%zu positions=%zu nonnull=%zu deep=%zu states=%u records=%u chains=%zu\n",
-                fd.pats.size(), text.size(), nonnull, deep, dfa.states, im.nrec, chains);
+    std::printf("ok patterns=%zu positions=%zu nonnull=%zu deep=%zu states=%u records=%u\n",
+                fd.pats.size(), text.size(), nonnull, deep, dfa.states, im.nrec);
     return 0;
 }

@@ -95,13 +95,6 @@ def rec_walk(rec, text, p, avail, node, d):
         R = rec[node]
         if d >= avail:
             return int(R[9])
-        if int(R[11]) == 0xFFFFFFFF:  # chain record: the whole unary path or the answer so far
-            L = int(R[10])
-            if L > avail - d or any(int(text[p - d - j]) != (int(R[(15 - j) >> 2]) >> (8 * ((15 - j) & 3))) & 0xFF
-                                    for j in range(L)):
-                return int(R[9])
-            node, d = int(R[8]), d + L
-            continue
         c = int(text[p - d])
         w, bit = c >> 5, c & 31
         if not (int(R[w]) >> bit) & 1:
