@@ -776,30 +776,48 @@ __global__ __launch_bounds__(SCORE_THREADS) void score_kernel(const uint32_t* __
 // the u64 global histogram (nonzero counters only) at the end.
 constexpr int HIST_THREADS = 1024;
 constexpr uint32_t HIST_WINDOW = 38912;  // 152 KiB of u32 counters
+constexpr int HIST_V = 4;  // 16-B answer loads per thread per step (snort 1 GiB: V=1/2/4/8 2.07/1.49/1.29/1.30 ms; one chain at a time 3.66)
 
+// Each thread takes V 16-B loads of answers (4V positions) and walks their 4V
+// suffix chains together, so the dependent parent[] gathers of one step are
+// all in flight at once (one chain after another left them latency-bound).
+template <int V>
 __global__ __launch_bounds__(HIST_THREADS) void hist_kernel(const uint32_t* __restrict__ real, int64_t n,
                                                             const uint32_t* __restrict__ parent, uint32_t lo,
                                                             uint32_t cnt, unsigned long long* __restrict__ hist) {
     __shared__ uint32_t s_h[HIST_WINDOW];
     for (uint32_t k = threadIdx.x; k < cnt; k += HIST_THREADS) s_h[k] = 0;
     __syncthreads();
-    auto add = [&](uint32_t g) {
-        while (g) {
-            if (g - lo < cnt) atomicAdd(&s_h[g - lo], 1u);
-            g = parent[g];
-        }
-    };
     using v4 = __attribute__((ext_vector_type(4))) unsigned int;
     const int64_t nv = n / 4;
     const int64_t stride = (int64_t)gridDim.x * HIST_THREADS;
-    for (int64_t k = (int64_t)blockIdx.x * HIST_THREADS + threadIdx.x; k < nv; k += stride) {
-        const v4 r = __builtin_nontemporal_load(reinterpret_cast<const v4*>(real) + k);
-        add(r.x);
-        add(r.y);
-        add(r.z);
-        add(r.w);
+    for (int64_t k = (int64_t)blockIdx.x * HIST_THREADS + threadIdx.x; k < nv; k += V * stride) {
+        uint32_t g[4 * V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int64_t kj = k + j * stride;
+            const v4 r = kj < nv ? __builtin_nontemporal_load(reinterpret_cast<const v4*>(real) + kj) : v4{0, 0, 0, 0};
+            g[4 * j] = r.x;
+            g[4 * j + 1] = r.y;
+            g[4 * j + 2] = r.z;
+            g[4 * j + 3] = r.w;
+        }
+        for (;;) {
+            uint32_t any = 0;
+#pragma unroll
+            for (int i = 0; i < 4 * V; ++i) any |= g[i];
+            if (!any) break;
+#pragma unroll
+            for (int i = 0; i < 4 * V; ++i)
+                if (g[i] - lo < cnt) atomicAdd(&s_h[g[i] - lo], 1u);
+#pragma unroll
+            for (int i = 0; i < 4 * V; ++i) g[i] = g[i] ? parent[g[i]] : 0u;
+        }
     }
-    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) add(real[4 * nv + threadIdx.x]);
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        for (uint32_t g = real[4 * nv + threadIdx.x]; g; g = parent[g])
+            if (g - lo < cnt) atomicAdd(&s_h[g - lo], 1u);
+    }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < cnt; k += HIST_THREADS)
         if (s_h[k]) atomicAdd(hist + lo + k, (unsigned long long)s_h[k]);
@@ -927,7 +945,8 @@ hipError_t pm_launch_pattern_counts(const uint32_t* real, int64_t n, const uint3
     if (blocks < 1) blocks = 1;
     for (uint32_t lo = 1; lo < n_gids; lo += HIST_WINDOW) {
         const uint32_t cnt = n_gids - lo < HIST_WINDOW ? n_gids - lo : HIST_WINDOW;
-        hipLaunchKernelGGL(hist_kernel, dim3((unsigned)blocks), dim3(HIST_THREADS), 0, s, real, n, parent, lo, cnt, hist);
+        hipLaunchKernelGGL(hist_kernel<HIST_V>, dim3((unsigned)blocks), dim3(HIST_THREADS), 0, s, real, n, parent,
+                           lo, cnt, hist);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
