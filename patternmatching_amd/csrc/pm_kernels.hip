@@ -743,6 +743,9 @@ __device__ __forceinline__ void score_one(uint32_t a, uint32_t r, const uint32_t
 
 constexpr int SCORE_THREADS = 256;
 
+// V pairs of 16-B loads per thread before scoring them (1 GiB: V=1 1.78 ms, V=2 1.69 ms).
+constexpr int SCORE_V = 2;
+template <int V>
 __global__ __launch_bounds__(SCORE_THREADS) void score_kernel(const uint32_t* __restrict__ algo,
                                                               const uint32_t* __restrict__ real, int64_t n,
                                                               const uint32_t* __restrict__ parent,
@@ -754,12 +757,22 @@ __global__ __launch_bounds__(SCORE_THREADS) void score_kernel(const uint32_t* __
     using v4 = __attribute__((ext_vector_type(4))) unsigned int;
     const v4* A = reinterpret_cast<const v4*>(algo);
     const v4* R = reinterpret_cast<const v4*>(real);
-    for (int64_t k = (int64_t)blockIdx.x * SCORE_THREADS + threadIdx.x; k < nv; k += stride) {
-        const v4 a = __builtin_nontemporal_load(A + k), r = __builtin_nontemporal_load(R + k);
-        score_one(a.x, r.x, parent, depth, c);
-        score_one(a.y, r.y, parent, depth, c);
-        score_one(a.z, r.z, parent, depth, c);
-        score_one(a.w, r.w, parent, depth, c);
+    for (int64_t k = (int64_t)blockIdx.x * SCORE_THREADS + threadIdx.x; k < nv; k += V * stride) {
+        v4 a[V], r[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int64_t kj = k + j * stride;
+            a[j] = kj < nv ? __builtin_nontemporal_load(A + kj) : v4{0, 0, 0, 0};
+            r[j] = kj < nv ? __builtin_nontemporal_load(R + kj) : v4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            if (k + j * stride >= nv) break;
+            score_one(a[j].x, r[j].x, parent, depth, c);
+            score_one(a[j].y, r[j].y, parent, depth, c);
+            score_one(a[j].z, r[j].z, parent, depth, c);
+            score_one(a[j].w, r[j].w, parent, depth, c);
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x < (n & 3)) score_one(algo[4 * nv + threadIdx.x], real[4 * nv + threadIdx.x], parent, depth, c);
 #pragma unroll
@@ -932,8 +945,8 @@ hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n
     int64_t blocks = (n / 4 + SCORE_THREADS - 1) / SCORE_THREADS;
     if (blocks > (int64_t)num_cu * 8) blocks = (int64_t)num_cu * 8;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(score_kernel, dim3((unsigned)blocks), dim3(SCORE_THREADS), 0, s, algo, real, n, parent, depth,
-                       counts);
+    hipLaunchKernelGGL(score_kernel<SCORE_V>, dim3((unsigned)blocks), dim3(SCORE_THREADS), 0, s, algo, real, n, parent,
+                       depth, counts);
     return hipGetLastError();
 }
 
