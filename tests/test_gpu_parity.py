@@ -529,3 +529,45 @@ def test_adversarial_stream_large_rt_equals_ac():
     o.reset()
     exp = o.scan_codes(text[:1 << 20])
     assert np.array_equal(rt._codes[a[:1 << 20].cpu().numpy().view(np.uint32)], exp)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 17, 4099, (1 << 18) * 4 + 13])
+def test_score_and_counts_ragged_lengths(n):
+    """Both A12 kernels load several 16-B id vectors per thread (HIST_V,
+    SCORE_V in csrc/pm_kernels.hip) and score the n % 4 tail separately; tiny
+    and ragged lengths against the numpy restatement (measure.c:174-190)."""
+    torch = _torch()
+    s = torch.cuda.current_stream().cuda_stream
+    rt = matcher("snort", "rt")
+    P = rt.lib.pm_hip_n_patterns(rt.obj)
+    parent = np.array([rt.parent_gid(g) for g in range(P + 1)], np.int64)
+    depth = np.zeros(P + 1, np.int64)
+    for g in range(1, P + 1):
+        c, k = g, 0
+        while c:
+            c, k = parent[c], k + 1
+        depth[g] = k
+    rng = np.random.default_rng(n)
+    real = rng.integers(0, P + 1, n).astype(np.uint32)
+    real[rng.random(n) < 0.3] = 0
+    algo = real.copy()
+    m = rng.random(n)
+    algo[m < 0.1] = 0
+    algo[(m >= 0.1) & (m < 0.2)] = parent[real[(m >= 0.1) & (m < 0.2)]].astype(np.uint32)
+    algo[m >= 0.9] = rng.integers(1, P + 1, int((m >= 0.9).sum()))
+    pad = np.zeros(4, np.uint32)
+    ad = torch.from_numpy(np.concatenate([algo, pad]).view(np.int32)).cuda()
+    rd = torch.from_numpy(np.concatenate([real, pad]).view(np.int32)).cuda()
+    cnt = torch.zeros(5, dtype=torch.int64, device="cuda")
+    rt.score_device(ad.data_ptr(), rd.data_ptr(), n, cnt.data_ptr(), s)
+    hist = torch.zeros(P + 1, dtype=torch.int64, device="cuda")
+    rt.pattern_counts_device(rd.data_ptr(), n, hist.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert cnt.cpu().tolist() == _score_host(algo, real, parent, depth)
+    exp = np.zeros(P + 1, np.int64)
+    cur = real.astype(np.int64)
+    while cur.any():
+        cur = cur[cur > 0]
+        np.add.at(exp, cur, 1)
+        cur = parent[cur]
+    assert np.array_equal(hist.cpu().numpy(), exp)
