@@ -52,7 +52,9 @@ BfsTrie build_trie(const std::vector<std::string>& pats, const PmGidMap& g, bool
                 cur = it->second;
             }
         }
-        if (!p.empty() && gid[cur] == 0) gid[cur] = g.gid_of_index[k];
+        // a repeated byte string keeps the id added last, as ac_add_pattern
+        // does (mpac.c:272 `cur->id = id`); the earlier gid has no node
+        if (!p.empty()) gid[cur] = g.gid_of_index[k];
     }
     // children lists by creation id, sorted by byte
     std::vector<uint64_t> kids;  // (parent << 40) | (byte << 32) | child
@@ -89,6 +91,42 @@ BfsTrie build_trie(const std::vector<std::string>& pats, const PmGidMap& g, bool
         }
     }
     return t;
+}
+
+// The LDS filters are a function of t12, t3h and rec: stage 1 holds every
+// depth-3 key (every valid t3h entry); stage 2 the keys whose depth-3 node
+// is a pattern (its best-so-far differs from the depth-2 answer, gids being
+// unique per node) and every depth-4 suffix (the node's children: inline
+// bytes or its record's bitmap).  The build derives them this way and a
+// cached image must reproduce them exactly, so the filters can never drift
+// from the tables or the hash functions.
+std::vector<uint32_t> derive_filters(const RtImage& im) {
+    std::vector<uint32_t> filt(RT_FILTER_WORDS + RT_F2_WORDS, 0);
+    uint32_t* f2 = &filt[RT_FILTER_WORDS];
+    for (size_t e = 0; e + 3 < im.t3h.size(); e += 4) {
+        const uint32_t x = im.t3h[e], y = im.t3h[e + 1], z = im.t3h[e + 2], w = im.t3h[e + 3];
+        if (!(x & RT_T3H_VALID)) continue;
+        const uint32_t key = x & 0xFFFFFFu, kind = x >> 25;
+        const uint32_t f = pm_rt_fhash(key);
+        filt[pm_rt_filter_word(f)] |= pm_rt_filter_mask(f);
+        if ((key >> 8) < im.t12.size() && y != (im.t12[key >> 8] & (RT_CONT16 - 1))) {
+            const uint32_t g = pm_rt_p3hash(key);
+            f2[pm_rt_p3word(g)] |= pm_rt_filter_mask(g);
+        }
+        auto s4 = [&](uint32_t c) {
+            const uint32_t g = pm_rt_s4hash(c | (key << 8));
+            f2[pm_rt_s4word(g)] |= pm_rt_filter_mask(g);
+        };
+        if (kind == 1) {
+            for (uint32_t j = 0; j < (z >> 24) && j < RT_T3H_INLINE; ++j) s4((z >> (8 * j)) & 0xFFu);
+        } else if (kind == 2) {
+            const size_t r = (size_t)(w & ~RT_CONT32) * RT_REC_WORDS;
+            if (r + RT_REC_WORDS > im.rec.size()) continue;
+            for (uint32_t c = 0; c < 256; ++c)
+                if ((im.rec[r + (c >> 5)] >> (c & 31)) & 1u) s4(c);
+        }
+    }
+    return filt;
 }
 
 }  // namespace
@@ -152,8 +190,6 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
     uint32_t d3 = 0;
     for (uint32_t v = 1; v < t.n && t.depth[v] <= 2; ++v)
         if (t.depth[v] == 2) d3 += t.ccount[v];
-    im.filt.assign(RT_FILTER_WORDS + RT_F2_WORDS, 0);
-    uint32_t* f2 = &im.filt[RT_FILTER_WORDS];
     auto answer = [&](uint32_t v) { return t.ccount[v] ? (RT_CONT32 | (v - first_d3)) : best[v]; };
     std::vector<std::array<uint32_t, 4>> ents;
     ents.reserve(d3);
@@ -164,16 +200,6 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
             const uint32_t n3 = t.cstart[v] + k;
             const uint32_t c2 = t.label[n3];
             const uint32_t key = c2 | (c1 << 8) | (c0 << 16);
-            const uint32_t f = pm_rt_fhash(key);
-            im.filt[pm_rt_filter_word(f)] |= pm_rt_filter_mask(f);
-            if (t.gid[n3]) {  // a 3-byte pattern
-                const uint32_t g = pm_rt_p3hash(key);
-                f2[pm_rt_p3word(g)] |= pm_rt_filter_mask(g);
-            }
-            for (uint32_t q = 0; q < t.ccount[n3]; ++q) {  // depth-4 suffixes
-                const uint32_t g = pm_rt_s4hash(t.label[t.cstart[n3] + q] | (key << 8));
-                f2[pm_rt_s4word(g)] |= pm_rt_filter_mask(g);
-            }
             std::array<uint32_t, 4> e{};
             const uint32_t nch = t.ccount[n3];
             const uint32_t kind = nch == 0 ? 0u : (nch <= RT_T3H_INLINE ? 1u : 2u);
@@ -235,6 +261,7 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
             pre += (uint32_t)__builtin_popcount(R[w]);
         }
     }
+    im.filt = derive_filters(im);
     return im;
 }
 
@@ -254,6 +281,11 @@ PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap&
         }
         best[v] = t.gid[v] ? t.gid[v] : up;
     }
+    // a gid shadowed by a later duplicate has no trie node and never appears
+    // in a scan: a root of its own (parent 0, depth 1) keeps the tables
+    // acyclic and depth == 1 + depth[parent] for every gid
+    for (size_t q = 1; q < r.depth.size(); ++q)
+        if (!r.depth[q]) r.depth[q] = 1;
     return r;
 }
 
@@ -288,7 +320,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 3;                     // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 4;                     // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);
@@ -399,6 +431,10 @@ bool values_ok(const PmImages& im, int kind, size_t ngid) {
         if (k == 1 && nch > 1 && (uint64_t)w + nch > rt.nrec) return false;
         if (k == 1 && nch == 1 && ((w & RT_CONT32) ? r >= rt.nrec : w > P)) return false;
         if (k == 2 && (!(w & RT_CONT32) || r >= rt.nrec)) return false;
+        // the entry sits in one of its key's two cuckoo slots (the device
+        // probes only those)
+        const uint32_t key = x & 0xFFFFFFu, sl = (uint32_t)(e / 4);
+        if (sl != pm_rt_slot1(key, rt.t3h_bits) && sl != pm_rt_slot2(key, rt.t3h_bits)) return false;
     }
     for (uint32_t n = 0; n < rt.nrec; ++n) {
         const uint32_t* R = &rt.rec[(size_t)n * RT_REC_WORDS];
@@ -410,7 +446,9 @@ bool values_ok(const PmImages& im, int kind, size_t ngid) {
         }
         if (pre && (uint64_t)R[8] + pre > rt.nrec) return false;
     }
-    return true;
+    // the LDS filters are exactly the ones the tables imply (no false
+    // negatives can hide in a damaged or stale filter word)
+    return rt.filt == derive_filters(rt);
 }
 
 }  // namespace
@@ -419,6 +457,23 @@ uint64_t pm_image_key(const std::vector<std::string>& pats, int kind) {
     uint64_t h = 0xCBF29CE484222325ull;
     const uint32_t v[2] = {IMG_VERSION, (uint32_t)kind};
     h = fnv1a(h, v, sizeof v);
+    // layout constants and the hash functions themselves (their values on a
+    // few keys): a change to either gives new keys, not a stale hit
+    uint32_t lay[] = {RT_T1_BASE, RT_CONT16, RT_CONT32, (uint32_t)RT_REC_WORDS, RT_FILTER_WORDS, RT_F3_WORDS,
+                      RT_F4_WORDS, RT_T3H_INLINE, RT_T3H_VALID, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t probe[2] = {0x00A1B2C3u, 0x00FFFFFFu};
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t k = probe[q];
+        uint32_t* o = &lay[9 + 7 * q];
+        o[0] = pm_rt_fhash(k);
+        o[1] = pm_rt_filter_mask(o[0]) ^ pm_rt_filter_word(o[0]);
+        o[2] = pm_rt_p3hash(k) ^ pm_rt_p3word(pm_rt_p3hash(k));
+        o[3] = pm_rt_s4hash(k << 8 | 0x5A) ^ pm_rt_s4word(pm_rt_s4hash(k << 8 | 0x5A));
+        o[4] = pm_rt_slot1(k, 20);
+        o[5] = pm_rt_slot2(k, 20);
+        o[6] = pm_rt_hash(k);
+    }
+    h = fnv1a(h, lay, sizeof lay);
     for (const auto& p : pats) {
         const uint64_t n = p.size();
         h = fnv1a(h, &n, 8);

@@ -87,8 +87,9 @@ struct PmParents {
     std::vector<uint32_t> parent, depth;
 };
 
-// Patterns are given in add_pattern order; duplicates are not expected (the
-// host front end de-duplicates) but are tolerated: the first one wins.
+// Patterns are given in add_pattern order.  The host front end de-duplicates
+// (PatternsTree.c:193-196), but a plugin caller may repeat a byte string: as
+// in ac_add_pattern (mpac.c:272) the id added last wins.
 PmGidMap pm_assign_gids(const std::vector<std::string>& pats);
 RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g);
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g);
@@ -96,10 +97,11 @@ PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap&
 
 // Compiled-image cache: the flattened tables of a
 // dictionary, on disk, keyed by a hash of the patterns in add order and the
-// image kind.  pm_image_key hashes (format version, kind, every pattern's
-// length and bytes).  Files are written to a temporary name and renamed, so
+// image kind.  pm_image_key hashes (format version, kind, the layout
+// constants and hash functions below, every pattern's length and bytes).  Files are written to a temporary name and renamed, so
 // a reader never sees a partial file; anything that does not validate
-// (magic, key, kind, section sizes) is ignored and rebuilt.
+// (magic, key, kind, section sizes, every index and gid, the cuckoo slots,
+// and filters equal to the ones the tables imply) is ignored and rebuilt.
 struct PmImages {
     RtImage rt;
     DfaImage dfa;

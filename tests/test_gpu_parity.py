@@ -143,6 +143,19 @@ def test_read_block_returns_pattern_ids(kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
+def test_duplicate_add_pattern_last_id_wins(kind):
+    """add_pattern with a byte string already added: the later id is the one
+    returned, as ac_add_pattern overwrites `cur->id` (mpac.c:272)."""
+    m = pm.HipMatcher(kind)
+    m.add_pattern(b"abc", 0x1000)
+    m.add_pattern(b"bc", 0x2000)
+    m.add_pattern(b"abc", 0x3000)
+    m.compile()
+    assert m.read_block_ids(b"xxabcxbc") == [0, 0, 0, 0, 0x3000, 0, 0, 0x2000]
+    m.free()
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_empty_and_ragged_inputs(kind):
     m = matcher("snort", kind)
     assert m.read_block_codes(b"").size == 0

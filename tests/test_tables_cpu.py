@@ -158,6 +158,44 @@ def test_compiled_image_cache(tmp_path):
     assert not list(tmp_path.glob("*.tmp.*"))
 
 
+def test_compiled_image_cache_rejects_a_damaged_filter(tmp_path):
+    """a cached RT image whose LDS filter words differ from the
+    ones its tables imply (a cleared bit = silent misses) is rebuilt."""
+    pats = pm.Dictionary(dict_paths("et")).patterns()
+    a = FlatImage(pats, pm.KIND_RT, tmp_path)
+    (f,) = tmp_path.glob(f"pm-{pm.KIND_RT}-*.img")
+    raw = bytearray(f.read_bytes())
+    # header 24 B; sections: 16-B header + data (scal 7 u32, t12 u16[65792], filt)
+    off = 24 + 16 + 28 + 16 + 2 * 65792 + 16
+    filt = np.frombuffer(bytes(raw[off:off + 4 * 4096]), np.uint32)
+    assert np.array_equal(filt, a.array("filt")[:4096])
+    w = int(np.nonzero(filt)[0][0])
+    word = int(filt[w])
+    raw[off + 4 * w:off + 4 * w + 4] = (word & (word - 1)).to_bytes(4, "little")
+    f.write_bytes(bytes(raw))
+    b = FlatImage(pats, pm.KIND_RT, tmp_path)
+    assert not b.cache_hit and np.array_equal(b.array("filt"), a.array("filt"))
+    assert FlatImage(pats, pm.KIND_RT, tmp_path).cache_hit
+
+
+def test_duplicate_pattern_last_id_wins_and_caches(tmp_path):
+    """a byte string added twice keeps the id added last, as
+    ac_add_pattern does (mpac.c:272 `cur->id = id`); the shadowed gid is a
+    root of its own, so the image still validates and caches."""
+    pats = [b"abc", b"bc", b"abc", b"zq"]
+    text = np.frombuffer(b"xxabcxzqbc", np.uint8)
+    for kind in (pm.KIND_RT, pm.KIND_AC):
+        img = FlatImage(pats, kind, tmp_path)
+        assert not img.cache_hit
+        assert FlatImage(pats, kind, tmp_path).cache_hit
+        idx = img.array("index_of_gid")
+        gids = rt_scan(img, text) if kind == pm.KIND_RT else dfa_scan(img, text)
+        assert [int(idx[g]) if g else -1 for g in gids] == [-1, -1, -1, -1, 2, -1, -1, 3, -1, 1]
+        parent, depth = img.array("parent"), img.array("depth")
+        shadowed = int(np.nonzero(idx == 0)[0][1])  # gid of index 0 (idx[0] is the unused slot)
+        assert parent[shadowed] == 0 and depth[shadowed] == 1
+
+
 def test_rt_image_context():
     """Positions scanned with only max_len-1 bytes of context are exact."""
     d, img, tab = image("merged", pm.KIND_RT)
