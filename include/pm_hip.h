@@ -137,12 +137,12 @@ int pm_hip_device_count(void);
 int pm_hip_set_device(int device);
 
 /* Timing-only ablation launches of the reverse-trie kernel (variant 0 =
- * product kernel, 1 = no depth>=3 stage, 2 = streaming only, 9 = product
- * kernel with per-phase cycle stamps summed into d_count[0..7]); out_width
- * 4 / 2 = u32 / u16 ids (d_out may be NULL: count only); blocks <= 0 keeps
- * the default grid.  Outputs of variants 1-2 are not match ids. */
+ * product kernel, 1 = no depth>=3 stage, 2 = streaming only, 3 = product
+ * kernel with one deep walk per lane after the chunk loop); out_width
+ * 4 / 2 = u32 / u16 ids (d_out may be NULL: count only).  Outputs of
+ * variants 1-2 are not match ids; variant 3's are. */
 int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out,
-                              int out_width, unsigned long long* d_count, void* hip_stream, int blocks);
+                              int out_width, unsigned long long* d_count, void* hip_stream);
 /* Launch shape of the AC-DFA kernel for timing sweeps: segments in flight
  * (lanes) per CU; 0 restores the default. */
 void pm_hip_debug_dfa_shape(int lanes_per_cu);

@@ -104,7 +104,7 @@ SIGNATURES = {
     "pm_hip_device_count": (ctypes.c_int, []),
     "pm_hip_set_device": (ctypes.c_int, [ctypes.c_int]),
     "pm_hip_debug_scan_variant": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int64, c_vp, ctypes.c_int,
-                                                 c_vp, c_vp, ctypes.c_int]),
+                                                 c_vp, c_vp]),
     "pm_hip_debug_dfa_shape": (None, [ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),

@@ -122,8 +122,15 @@ std::vector<uint32_t> derive_filters(const RtImage& im) {
         } else if (kind == 2) {
             const size_t r = (size_t)(w & ~RT_CONT32) * RT_REC_WORDS;
             if (r + RT_REC_WORDS > im.rec.size()) continue;
-            for (uint32_t c = 0; c < 256; ++c)
-                if ((im.rec[r + (c >> 5)] >> (c & 31)) & 1u) s4(c);
+            const uint32_t* R = &im.rec[r];
+            const uint32_t rk = R[0] >> 30;
+            if (rk == RT_REC_KIDS) {
+                for (uint32_t j = 0; j < ((R[0] >> 24) & 63u) && j < RT_REC_INLINE; ++j) s4((R[2 + j / 4] >> (8 * (j & 3))) & 0xFFu);
+            } else if (rk == RT_REC_WIDE && (size_t)(R[2] + 1) * RT_WIDE_WORDS <= im.wide.size()) {
+                const uint32_t* W = &im.wide[(size_t)R[2] * RT_WIDE_WORDS];
+                for (uint32_t c = 0; c < 256; ++c)
+                    if ((W[pm_rt_wide_word(c >> 5)] >> (c & 31)) & 1u) s4(c);
+            }
         }
     }
     return filt;
@@ -168,7 +175,8 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
     im.nrec = t.n - first_d3;
     uint32_t max_len = 0;
     for (const auto& p : pats) max_len = std::max<uint32_t>(max_len, (uint32_t)p.size());
-    im.fits = n_short < RT_CONT16 && im.nrec < (1u << 22) && max_len <= 512;
+    im.fits = n_short < RT_CONT16 && im.nrec < (1u << 23) && max_len <= 511;
+    // (nwide < 2^14 is checked after the records are built)
     if (!im.fits) return im;
 
     im.t12.assign(RT_T1_BASE + 256, 0);
@@ -246,20 +254,40 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
         }
         if (ok) break;
     }
+    // 16-B node records (pm_flatten.h): children inline up to RT_REC_INLINE,
+    // else a 64-B bitmap-rank entry in `wide`
     im.rec.assign((size_t)im.nrec * RT_REC_WORDS, 0);
+    im.nwide = 0;
     for (uint32_t v = first_d3; v < t.n; ++v) {
         uint32_t* R = &im.rec[(size_t)(v - first_d3) * RT_REC_WORDS];
-        for (uint32_t k = 0; k < t.ccount[v]; ++k) {
-            uint32_t c = t.label[t.cstart[v] + k];
-            R[c >> 5] |= 1u << (c & 31);
+        const uint32_t nch = t.ccount[v], first = nch ? t.cstart[v] - first_d3 : 0;
+        R[1] = best[v];
+        if (nch == 0) {
+            R[0] = RT_REC_LEAF << 30;
+        } else if (nch <= RT_REC_INLINE) {
+            R[0] = (RT_REC_KIDS << 30) | (nch << 24) | first;
+            for (uint32_t j = 0; j < nch; ++j) R[2 + j / 4] |= (uint32_t)t.label[t.cstart[v] + j] << (8 * (j & 3));
+        } else {
+            R[0] = (RT_REC_WIDE << 30) | first;
+            R[2] = im.nwide++;
+            const size_t base = im.wide.size();
+            im.wide.resize(base + RT_WIDE_WORDS, 0);
+            uint32_t* W = &im.wide[base];
+            for (uint32_t k = 0; k < nch; ++k) {
+                const uint32_t c = t.label[t.cstart[v] + k];
+                W[pm_rt_wide_word(c >> 5)] |= 1u << (c & 31);
+            }
+            uint32_t idx = first;
+            for (int q = 0; q < 4; ++q) {  // quarter q: words 2q, 2q+1
+                W[4 * q + 2] = idx;
+                W[4 * q + 3] = best[v];
+                idx += (uint32_t)__builtin_popcount(W[4 * q]) + (uint32_t)__builtin_popcount(W[4 * q + 1]);
+            }
         }
-        R[8] = t.ccount[v] ? t.cstart[v] - first_d3 : 0;
-        R[9] = best[v];
-        uint32_t pre = 0;
-        for (int w = 0; w < 8; ++w) {
-            R[10 + (w >> 2)] |= pre << (8 * (w & 3));
-            pre += (uint32_t)__builtin_popcount(R[w]);
-        }
+    }
+    if (im.nwide >= (1u << 14)) {  // a queued wide step holds the entry in 14 bits
+        im.fits = false;
+        return im;
     }
     im.filt = derive_filters(im);
     return im;
@@ -320,7 +348,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 4;                     // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 6;                     // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);
@@ -352,11 +380,11 @@ bool save(const std::string& path, uint64_t key, int kind, const PmImages& im) {
     if (!f) return false;
     const uint32_t hdr[2] = {IMG_VERSION, (uint32_t)kind};
     const std::vector<uint32_t> scal = {im.rt.fits ? 1u : 0u, im.rt.t3h_bits, im.rt.n2int, im.rt.nrec, im.rt.nodes,
-                                        im.rt.d3, im.dfa.states};
+                                        im.rt.d3, im.dfa.states, im.rt.nwide};
     bool ok = std::fwrite(&IMG_MAGIC, 8, 1, f) == 1 && std::fwrite(&key, 8, 1, f) == 1 && std::fwrite(hdr, 4, 2, f) == 2 &&
               put(f, 1, scal) && put(f, 2, im.rt.t12) && put(f, 3, im.rt.filt) && put(f, 4, im.rt.t3h) &&
               put(f, 5, im.rt.rec) && put(f, 6, im.dfa.next) && put(f, 7, im.dfa.out) && put(f, 8, im.par.parent) &&
-              put(f, 9, im.par.depth);
+              put(f, 9, im.par.depth) && put(f, 10, im.rt.wide);
     ok = (std::fclose(f) == 0) && ok;
     if (ok) ok = std::rename(tmp.c_str(), path.c_str()) == 0;
     if (!ok) std::remove(tmp.c_str());
@@ -371,9 +399,9 @@ bool load(const std::string& path, uint64_t key, int kind, PmImages& im) {
     std::vector<uint32_t> scal;
     bool ok = std::fread(&magic, 8, 1, f) == 1 && std::fread(&k, 8, 1, f) == 1 && std::fread(hdr, 4, 2, f) == 2 &&
               magic == IMG_MAGIC && k == key && hdr[0] == IMG_VERSION && hdr[1] == (uint32_t)kind &&
-              get(f, 1, scal) && scal.size() == 7 && get(f, 2, im.rt.t12) && get(f, 3, im.rt.filt) &&
+              get(f, 1, scal) && scal.size() == 8 && get(f, 2, im.rt.t12) && get(f, 3, im.rt.filt) &&
               get(f, 4, im.rt.t3h) && get(f, 5, im.rt.rec) && get(f, 6, im.dfa.next) && get(f, 7, im.dfa.out) &&
-              get(f, 8, im.par.parent) && get(f, 9, im.par.depth);
+              get(f, 8, im.par.parent) && get(f, 9, im.par.depth) && get(f, 10, im.rt.wide);
     char extra;
     ok = ok && std::fread(&extra, 1, 1, f) == 0;  // nothing after the last section
     std::fclose(f);
@@ -385,11 +413,13 @@ bool load(const std::string& path, uint64_t key, int kind, PmImages& im) {
     im.rt.nodes = scal[4];
     im.rt.d3 = scal[5];
     im.dfa.states = scal[6];
+    im.rt.nwide = scal[7];
     // structural checks: the kernels index these tables without bounds
     if (kind == 1 && im.rt.fits &&
         (im.rt.t12.size() != RT_T1_BASE + 256 || im.rt.filt.size() != RT_FILTER_WORDS + RT_F2_WORDS ||
          im.rt.t3h_bits < 4 || im.rt.t3h_bits > 30 || im.rt.t3h.size() != ((size_t)4 << im.rt.t3h_bits) ||
-         im.rt.rec.size() != (size_t)im.rt.nrec * RT_REC_WORDS))
+         im.rt.rec.size() != (size_t)im.rt.nrec * RT_REC_WORDS ||
+         im.rt.wide.size() != (size_t)im.rt.nwide * RT_WIDE_WORDS))
         return false;
     if (kind == 2 && (im.dfa.next.size() != (size_t)im.dfa.states * 256 || im.dfa.out.size() != im.dfa.states))
         return false;
@@ -419,7 +449,7 @@ bool values_ok(const PmImages& im, int kind, size_t ngid) {
     }
     const RtImage& rt = im.rt;
     if (!rt.fits) return true;
-    if (rt.nrec >= (1u << 22)) return false;
+    if (rt.nrec >= (1u << 23) || rt.nwide >= (1u << 14)) return false;
     for (uint16_t x : rt.t12)
         if ((x & 0x7FFFu) > P) return false;
     for (size_t e = 0; e < rt.t3h.size(); e += 4) {
@@ -436,15 +466,25 @@ bool values_ok(const PmImages& im, int kind, size_t ngid) {
         const uint32_t key = x & 0xFFFFFFu, sl = (uint32_t)(e / 4);
         if (sl != pm_rt_slot1(key, rt.t3h_bits) && sl != pm_rt_slot2(key, rt.t3h_bits)) return false;
     }
+    // records: children strictly after their parent (BFS), so every walk
+    // terminates; indices in range; wide entries' prefix counts consistent
     for (uint32_t n = 0; n < rt.nrec; ++n) {
         const uint32_t* R = &rt.rec[(size_t)n * RT_REC_WORDS];
-        if (R[9] > P) return false;
-        uint32_t pre = 0;
-        for (int w = 0; w < 8; ++w) {
-            if (((R[10 + (w >> 2)] >> (8 * (w & 3))) & 0xFFu) != pre) return false;
-            pre += (uint32_t)__builtin_popcount(R[w]);
+        const uint32_t rk = R[0] >> 30, cnt = (R[0] >> 24) & 63u, first = R[0] & 0xFFFFFFu;
+        if (R[1] > P) return false;
+        if (rk == RT_REC_LEAF) continue;
+        if (rk == RT_REC_KIDS) {
+            if (cnt < 1 || cnt > RT_REC_INLINE || first <= n || (uint64_t)first + cnt > rt.nrec) return false;
+            continue;
         }
-        if (pre && (uint64_t)R[8] + pre > rt.nrec) return false;
+        if (rk != RT_REC_WIDE || R[2] >= rt.nwide || first <= n) return false;
+        const uint32_t* W = &rt.wide[(size_t)R[2] * RT_WIDE_WORDS];
+        uint64_t idx = first;
+        for (int q = 0; q < 4; ++q) {
+            if (W[4 * q + 2] != idx || W[4 * q + 3] != R[1]) return false;
+            idx += (uint32_t)__builtin_popcount(W[4 * q]) + (uint32_t)__builtin_popcount(W[4 * q + 1]);
+        }
+        if (idx - first <= RT_REC_INLINE || idx > rt.nrec) return false;
     }
     // the LDS filters are exactly the ones the tables imply (no false
     // negatives can hide in a damaged or stale filter word)
@@ -460,7 +500,8 @@ uint64_t pm_image_key(const std::vector<std::string>& pats, int kind) {
     // layout constants and the hash functions themselves (their values on a
     // few keys): a change to either gives new keys, not a stale hit
     uint32_t lay[] = {RT_T1_BASE, RT_CONT16, RT_CONT32, (uint32_t)RT_REC_WORDS, RT_FILTER_WORDS, RT_F3_WORDS,
-                      RT_F4_WORDS, RT_T3H_INLINE, RT_T3H_VALID, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                      RT_F4_WORDS, RT_T3H_INLINE, RT_T3H_VALID, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                      RT_REC_INLINE, (uint32_t)RT_WIDE_WORDS};
     const uint32_t probe[2] = {0x00A1B2C3u, 0x00FFFFFFu};
     for (int q = 0; q < 2; ++q) {
         const uint32_t k = probe[q];

@@ -37,9 +37,23 @@
 //                                           the first child (children are
 //                                           contiguous);
 //                                           kind 2: RT_CONT32 | n3's record
-//             rec   u32[nrec * 12]    48-B records for nodes of depth >= 3:
-//                                     child bitmap[8], child base, best, 8 u8
-//                                     prefix popcounts
+//             rec   u32x4[nrec]       16-B records for nodes of depth >= 3
+//                                     (BFS order, children contiguous):
+//                                       x = kind << 30 | count << 24 | first
+//                                           (kind RT_REC_LEAF: no children;
+//                                            RT_REC_KIDS: count <= 8 children,
+//                                            their bytes in z, w (byte j =
+//                                            child j, sorted), child j at
+//                                            record first + j;
+//                                            RT_REC_WIDE: more children, z =
+//                                            its `wide` entry)
+//                                       y = best pattern on the path to the node
+//             wide  u32[nwide * 16]   per wide node, 4 quarters of 16 B; quarter
+//                                     q = {bitmap word 2q, bitmap word 2q+1,
+//                                     first + children before word 2q, best}:
+//                                     one 16-B load decides a byte (child of
+//                                     byte c at that index + rank of c in the
+//                                     quarter's words)
 //  DfaImage the Aho-Corasick automaton of Core/src/mpac.c (goto + BFS
 //           failure links + suffix/output links, :147-210) flattened into a
 //           dense DFA: next[s*256 + c] and out[s] (gid of the longest pattern
@@ -60,15 +74,19 @@ struct PmGidMap {
 
 struct RtImage {
     // encodings fit: fewer than 32768 patterns of length <= 2 (u16 t12),
-    // records < 2^22 and patterns <= 512 bytes (queued deep-walk items)
+    // records < 2^23 and patterns < 512 bytes (a queued record step holds
+    // record | depth << 23)
     bool fits = false;
     std::vector<uint16_t> t12;
     std::vector<uint32_t> filt;
     std::vector<uint32_t> t3h;  // 4 words per entry
-    std::vector<uint32_t> rec;
+    std::vector<uint32_t> rec;   // 4 words per node of depth >= 3
+    std::vector<uint32_t> wide;  // RT_WIDE_WORDS per node with > RT_REC_INLINE children
     uint32_t t3h_bits = 0;
-    uint32_t n2int = 0, nrec = 0, nodes = 0, d3 = 0;
-    size_t bytes() const { return t12.size() * 2 + filt.size() * 4 + t3h.size() * 4 + rec.size() * 4; }
+    uint32_t n2int = 0, nrec = 0, nodes = 0, d3 = 0, nwide = 0;
+    size_t bytes() const {
+        return t12.size() * 2 + filt.size() * 4 + t3h.size() * 4 + rec.size() * 4 + wide.size() * 4;
+    }
 };
 
 struct DfaImage {
@@ -116,7 +134,11 @@ PmImages pm_build_images_cached(const std::vector<std::string>& pats, const PmGi
 constexpr uint32_t RT_T1_BASE = 65536;   // t12[65536 + c]: lookback of exactly one byte
 constexpr uint32_t RT_CONT16 = 0x8000u;  // t12: depth-2 node has children (low 15 bits: best so far)
 constexpr uint32_t RT_CONT32 = 0x80000000u;  // t3: continue at record (low 31 bits)
-constexpr int RT_REC_WORDS = 12;
+constexpr int RT_REC_WORDS = 4;
+constexpr uint32_t RT_REC_LEAF = 0, RT_REC_KIDS = 1, RT_REC_WIDE = 3;  // record kinds (x >> 30)
+constexpr uint32_t RT_REC_INLINE = 8;  // children held inline in a record
+constexpr int RT_WIDE_WORDS = 16;
+inline uint32_t pm_rt_wide_word(uint32_t w) { return 4 * (w >> 1) + (w & 1); }  // bitmap word w in an entry
 constexpr uint32_t RT_FILTER_WORDS = 4096;  // stage 1: 16 KiB of LDS
 constexpr uint32_t RT_F3_WORDS = 256;       // stage 2, 3-byte patterns: 1 KiB
 constexpr uint32_t RT_F4_WORDS = 1792;      // stage 2, depth-4 suffixes: 7 KiB

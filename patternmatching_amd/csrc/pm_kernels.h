@@ -7,12 +7,21 @@ constexpr size_t RT_SCRATCH_BYTES = 4096;
 
 struct RtDev {
     const uint16_t* t12;   // 65536 + 256 u16; the first 64K staged into LDS per workgroup
-    const uint32_t* filt;  // RT_FILTER_WORDS u32, staged into LDS per workgroup
+    const uint32_t* filt;  // RT_FILTER_WORDS + RT_F2_WORDS u32, staged into LDS per workgroup
     const uint4* t3h;      // 2^t3h_bits entries (pm_flatten.h)
-    const uint32_t* rec;   // nrec * 12
+    const uint4* rec;      // nrec 16-B node records
+    const uint4* wide;     // 4 quarters {word 2q, word 2q+1, child index, best} per wide node
     uint32_t* scratch;     // RT_SCRATCH_BYTES the kernel may overwrite (stand-in stores)
+    uint32_t* spill;       // spill_cap u32: per-wave regions of deep-walk items (scratch)
+    int64_t spill_cap;
+    int64_t spill_stride;  // set per launch
     uint32_t t3h_bits;
 };
+
+// Spill items (u32) an RT launch over n positions needs in RtDev::spill: one
+// per position of each wave's chunks.  Launches of any n reuse one buffer of
+// this size for n' <= n.
+int64_t pm_rt_spill_items(int64_t n, int num_cu);
 
 struct DfaDev {
     const uint32_t* next;  // states * 256
@@ -28,7 +37,7 @@ hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0,
 // ablation variants of the RT kernel (timing only; see pm_kernels.hip)
 hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
                                 void* out, int outw, unsigned long long* count, const RtDev& t, int num_cu,
-                                hipStream_t s, int blocks_override);
+                                hipStream_t s);
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s);
 // launch shape of the DFA kernel (timing sweeps): lanes per CU; <= 0

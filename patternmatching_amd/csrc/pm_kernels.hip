@@ -26,6 +26,8 @@
 //   (next[s*256+c], out[s]); one lane per stream segment, started from the
 //   root max_len-1 bytes before the segment (SURVEY.md §0.1 shard rule), so
 //   every segment is independent and exact.
+#include <type_traits>
+
 #include "pm_kernels.h"
 #include "pm_streamgen.h"
 
@@ -45,6 +47,7 @@ constexpr uint32_t CONT32 = 0x80000000u;
 constexpr uint32_t T3H_VALID = 1u << 24;
 constexpr uint32_t RT_POSMASK = (1u << 30) - 1;  // queue item: position - pos0
 constexpr uint32_t RT_SLOT2 = 1u << 30;          // queue item: probe t3h slot2
+constexpr uint32_t RT_REC_LEAF_K = 0, RT_REC_KIDS_K = 1, RT_REC_WIDE_K = 3;  // record kinds, must match pm_flatten.h
 
 __device__ __forceinline__ uint32_t rt_hash(uint32_t k) { return k * 0x9E3779B1u; }  // pm_rt_hash
 // pm_rt_fhash of the low 24 bits of k (the operand's top byte is ignored):
@@ -66,14 +69,6 @@ __device__ __forceinline__ uint32_t rt_fhit(uint32_t w, uint32_t f) {
     asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
         : "=v"(c) : "v"(f), "v"(w));
     return a & b & c & 1u;
-}
-
-__device__ __forceinline__ uint64_t stamp() {
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
 }
 
 // Stage 2 of the filter for q = text[i-3..i] (pm_rt_p3hash / pm_rt_s4hash):
@@ -108,21 +103,56 @@ __device__ __forceinline__ uint32_t wave_prefix(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Record walk.  `node` is a record reached after consuming text[i] ..
-// text[i-d+1]; avail = bytes that exist at or before i.
-// Each step loads the whole record and the next byte together.
-__device__ __forceinline__ uint32_t rt_deep(const uint8_t* __restrict__ text, const uint32_t* __restrict__ rec,
-                                            uint32_t node, int64_t i, int64_t avail, int64_t d) {
+// One record step (pm_flatten.h 16-B records): R = the record of the node
+// reached after text[i] .. text[i-d+1], c = text[i-d].  Returns the next
+// record, or -1 when the walk ends here (answer R.y).  A wide node's child
+// needs its `wide` entry W = {bitmap word, prefix} of word c >> 5.
+template <class V4>
+__device__ __forceinline__ uint32_t rec_kind(const V4& R) { return R.x >> 30; }
+// inline children: index of byte c among the record's cnt child bytes, or cnt
+// (the zero-byte test of payload ^ c*0x01010101: the lowest flagged byte is
+// exact; later flags are masked off by j < cnt, and bytes are distinct)
+template <class V4>
+__device__ __forceinline__ uint32_t rec_kid_index(const V4& R, uint32_t c) {
+    const uint32_t c4 = c * 0x01010101u;
+    const uint32_t lo = R.z ^ c4, hi = R.w ^ c4;
+    const uint32_t zl = (lo - 0x01010101u) & ~lo & 0x80808080u;
+    const uint32_t zh = (hi - 0x01010101u) & ~hi & 0x80808080u;
+    const uint32_t cnt = (R.x >> 24) & 63u;
+    const uint32_t j = zl ? (uint32_t)__builtin_ctz(zl) >> 3 : zh ? 4u + ((uint32_t)__builtin_ctz(zh) >> 3) : 8u;
+    return j < cnt ? j : cnt;
+}
+
+// A wide node's quarter Q = {word 2q, word 2q+1, child index of word 2q,
+// best} for byte c (q = c >> 6): the child's record, or ~0u when c is not
+// a child (the answer is then Q.w).
+template <class V4>
+__device__ __forceinline__ uint32_t wide_child(const V4& Q, uint32_t c) {
+    const uint32_t odd = (c >> 5) & 1u, bit = c & 31u;
+    const uint32_t word = odd ? Q.y : Q.x;
+    if (!((word >> bit) & 1u)) return ~0u;
+    return Q.z + (odd ? (uint32_t)__popc(Q.x) : 0u) + (uint32_t)__popc(word & ((1u << bit) - 1u));
+}
+
+// Record walk, one position (edge chunks): node = record reached after
+// consuming text[i] .. text[i-d+1]; avail = bytes at or before i.
+__device__ __forceinline__ uint32_t rt_deep(const uint8_t* __restrict__ text, const RtDev& t, uint32_t node, int64_t i,
+                                            int64_t avail, int64_t d) {
     for (;;) {
-        const uint32_t* R = rec + (size_t)node * 12;
-        const uint4 meta = *reinterpret_cast<const uint4*>(R + 8);  // {base, best, prefix}
-        if (d >= avail) return meta.y;
+        const uint4 R = t.rec[node];
+        if (d >= avail) return R.y;
         const uint32_t c = text[i - d];
-        const uint32_t w = c >> 5, bit = c & 31u;
-        const uint32_t word = R[w];
-        if (!((word >> bit) & 1u)) return meta.y;
-        const uint32_t pre = ((w < 4 ? meta.z : meta.w) >> (8 * (w & 3))) & 0xFFu;
-        node = meta.x + pre + __popc(word & ((1u << bit) - 1u));
+        const uint32_t kind = rec_kind(R), first = R.x & 0xFFFFFFu;
+        if (kind == RT_REC_LEAF_K) return R.y;
+        if (kind == RT_REC_KIDS_K) {
+            const uint32_t j = rec_kid_index(R, c);
+            if (j == ((R.x >> 24) & 63u)) return R.y;
+            node = first + j;
+        } else {
+            const uint32_t ch = wide_child(t.wide[(size_t)R.z * 4 + (c >> 6)], c);
+            if (ch == ~0u) return R.y;
+            node = ch;
+        }
         ++d;
     }
 }
@@ -149,11 +179,11 @@ __device__ __forceinline__ uint32_t rt_from_d2(const uint8_t* __restrict__ text,
         const uint32_t nch = e.z >> 24;
         const uint32_t k = c3 == (e.z & 0xFFu) ? 0u : c3 == ((e.z >> 8) & 0xFFu) ? 1u : c3 == ((e.z >> 16) & 0xFFu) ? 2u : 3u;
         if (k >= nch) return e.y;
-        if (nch > 1) return rt_deep(text, t.rec, e.w + k, i, avail, 4);
+        if (nch > 1) return rt_deep(text, t, e.w + k, i, avail, 4);
         if (!(e.w & CONT32)) return e.w;
-        return rt_deep(text, t.rec, e.w & 0x7FFFFFFFu, i, avail, 4);
+        return rt_deep(text, t, e.w & 0x7FFFFFFFu, i, avail, 4);
     }
-    return rt_deep(text, t.rec, e.w & 0x7FFFFFFFu, i, avail, 3);
+    return rt_deep(text, t, e.w & 0x7FFFFFFFu, i, avail, 3);
 }
 
 // One position, every boundary case (stream start, short lookback).
@@ -172,16 +202,6 @@ __device__ uint32_t rt_one(const uint8_t* __restrict__ text, const uint16_t* s_t
 // V (ablation, timing only; V=0 is the product kernel):
 //   1 = loads + t12 lookups + stores (no filter, no queue)
 //   2 = loads + stores only (streaming floor of this access pattern)
-//   3 = 2 plus a sleep per chunk, 4 = 2 plus ~500 dependent VALU per chunk
-//       (how the streaming rate tolerates per-chunk compute)
-//   5 = product kernel whose round loads all hit one line, 6 = product
-//       kernel without patch stores (both: wrong ids, timing only)
-//  10 = product kernel with sc1 (L2-dropping) chunk stores
-//  11 = t12 + stage-1 filter, no queue; 12 = + queue pushes, no rounds;
-//  13 = 11 + the push's DPP scan only (all: wrong ids, timing only)
-//   9 = product kernel with s_memtime stamps per phase (diagnostic: count
-//       receives 8 u64 cycle sums: lds+filter, push, round wait, consume,
-//       store, issue, chunks, total)
 // OUTW: bytes per written id: 4 (u32 gids, read_block), 2 (u16 gids, when
 // every gid < 65536), 0 (count only).
 template <int OUTW>
@@ -190,7 +210,211 @@ __device__ __forceinline__ void put_id(void* out, int64_t k, uint32_t v) {
     if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[k] = (uint16_t)v;
 }
 
-template <int VT, int OUTW>
+// Deep walks of one wave's spilled positions (items sp[0, sn): position -
+// pos0 | placeholder-nonzero << 31), after its chunk loop.  Every lane keeps
+// RT_TAIL_SLOTS walks in lock step, each one load per iteration (its
+// item, its 16-B text block, a t3h slot, a record, a wide quarter), so a wave
+// has 64 * RT_TAIL_SLOTS dependent chains in flight.  Each walk ends by
+// writing its answer and settling the count against its placeholder.
+constexpr int RT_TAIL_SLOTS = 4;
+enum : uint32_t { TS_EMPTY = 0, TS_ITEM, TS_KEY, TS_PROBE1, TS_PROBE2, TS_REC, TS_WIDE };
+
+// f(integral_constant<int, 0>) .. f(integral_constant<int, N-1>): a loop the
+// compiler sees fully unrolled with constant indices (per-slot state stays
+// in registers)
+template <int I, int N, class F>
+__device__ __forceinline__ void unroll_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        unroll_for<I + 1, N>(f);
+    }
+}
+
+using tu32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+// One in-flight walk.  Offsets are u32 from pos0; pa / pb are the next
+// iteration's load addresses (set when the state changes), so issuing is
+// two loads per slot whatever the state.
+struct TailSlot {
+    uint32_t st;          // TS_*
+    uint32_t pos;         // position - pos0 | placeholder-nonzero << 31
+    uint32_t av;          // bytes at or before the position, capped at 1024
+    uint32_t key;         // text[i-3..i] (LE); TS_WIDE: the byte c
+    uint32_t node, dd;    // record, depth (bytes consumed)
+    uint32_t tw;          // cached text dword
+    int32_t twa;          // its offset (dword-aligned, may precede pos0)
+    const tu32x4* pa;
+    const uint32_t* pb;
+    tu32x4 A;             // this iteration's 16-B load
+    uint32_t B;           // this iteration's dword load
+};
+
+template <int OUTW, int SLOTS = RT_TAIL_SLOTS>
+__device__ __forceinline__ void rt_tail(const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0,
+                                        void* __restrict__ out, const RtDev& t, const uint32_t* s_f2,
+                                        const uint32_t* sp, uint32_t sn, int lane, uint32_t& cnt) {
+    const uint8_t* const tb = text + pos0;  // offsets are from pos0; pos0 % 16 == 0
+    const int64_t ctx64 = pos0 - stream_start;  // context bytes before pos0
+    const uint32_t ctx = ctx64 > 1024 ? 1024u : (uint32_t)ctx64;
+    const tu32x4* const dummy4 = reinterpret_cast<const tu32x4*>(t.filt);
+    const uint32_t* const dummy1 = t.filt;
+    const tu32x4* const T3 = reinterpret_cast<const tu32x4*>(t.t3h);
+    const tu32x4* const RC = reinterpret_cast<const tu32x4*>(t.rec);
+    const tu32x4* const WD = reinterpret_cast<const tu32x4*>(t.wide);
+    TailSlot S[SLOTS];
+    unroll_for<0, SLOTS>([&](auto I) __attribute__((always_inline)) {
+        TailSlot& z = S[I];
+        z.st = TS_EMPTY;
+        z.pos = z.av = z.key = z.node = z.dd = z.tw = z.B = 0;
+        z.twa = 0;
+        z.pa = dummy4;
+        z.pb = dummy1;
+        z.A = tu32x4{0u, 0u, 0u, 0u};
+    });
+    uint32_t nxt = 0;  // wave-uniform: next unclaimed item
+    for (;;) {
+        // refill empty slots with the next items, in item order across lanes
+        bool busy = false;
+        unroll_for<0, SLOTS>([&](auto I) __attribute__((always_inline)) {
+            TailSlot& z = S[I];
+            const bool need = z.st == TS_EMPTY;
+            const uint64_t m = __ballot(need);
+            const uint32_t idx = nxt + wave_prefix(m);
+            if (need && idx < sn) {
+                z.st = TS_ITEM;
+                z.pa = dummy4;
+                z.pb = sp + idx;
+            }
+            nxt += (uint32_t)__popcll(m);
+            if (nxt > sn) nxt = sn;
+            busy |= z.st != TS_EMPTY;
+        });
+        if (!__ballot(busy)) break;  // wave-uniform
+        // issue: every slot's two loads in flight together
+        unroll_for<0, SLOTS>([&](auto I) __attribute__((always_inline)) {
+            TailSlot& z = S[I];
+            z.A = *z.pa;
+            z.B = *z.pb;
+        });
+        // resolve, branch-free: every state's outcome is computed and the
+        // slot's own selected (divergent branches per state cost more than
+        // the arithmetic: exec-mask bookkeeping and register merges)
+        unroll_for<0, SLOTS>([&](auto I) __attribute__((always_inline)) {
+            TailSlot& z = S[I];
+            const uint32_t st = z.st;
+            const tu32x4 A = z.A;
+            const uint32_t off = z.pos & RT_POSMASK;
+            // TS_ITEM: B is the item
+            const uint32_t io = z.B & RT_POSMASK, iob = io & ~15u;
+            // TS_KEY: text[i-3..i] from the 20-byte window {dword before
+            // the block, the block}.  Bit-test select tree: an equality chain
+            // over the vector's components compiles to a dynamic extract,
+            // measured wrong for q = 3 on gfx950.
+            const uint32_t q = (off >> 2) & 3u, b = off & 3u;
+            const uint32_t h01 = (q & 1) ? A.y : A.x, h23 = (q & 1) ? A.w : A.z;
+            const uint32_t l01 = (q & 1) ? A.x : z.B, l23 = (q & 1) ? A.z : A.y;
+            const uint32_t hi = (q & 2) ? h23 : h01, lo = (q & 2) ? l23 : l01;
+            const uint32_t k32 = b == 3 ? hi : __builtin_amdgcn_alignbit(hi, lo, 8 * (b + 1));
+            const bool s2 = rt_stage2_hit(rt_stage2_load(s_f2, k32)) != 0u;
+            // TS_PROBE1/2: A is the t3h slot of key >> 8
+            const uint32_t key = z.key;
+            const bool match = (A.x & 0x1FFFFFFu) == (T3H_VALID | (key >> 8));
+            const uint32_t kind3 = A.x >> 25, nch = A.z >> 24, c3 = key & 0xFFu;
+            const uint32_t j3 = c3 == (A.z & 0xFFu) ? 0u : c3 == ((A.z >> 8) & 0xFFu) ? 1u
+                              : c3 == ((A.z >> 16) & 0xFFu) ? 2u : 3u;
+            const bool deep4 = z.av >= 4;
+            const bool inl = kind3 == 1 && j3 < nch && nch == 1 && !(A.w & CONT32);  // the child's answer inline
+            const bool pwalk = match && deep4 && ((kind3 == 1 && j3 < nch && !inl) || kind3 == 2);
+            const uint32_t pnode = (kind3 == 2 || nch == 1) ? A.w & 0x7FFFFFFFu : A.w + j3;
+            const uint32_t pans = (match && deep4 && inl) ? A.w : A.y;
+            const bool pslot2 = !match && (A.x & T3H_VALID) && st == TS_PROBE1;
+            // TS_REC: A is the record, B the text dword when reloaded
+            const int32_t rq = (int32_t)off - (int32_t)z.dd;
+            const bool reload = rq < z.twa || rq >= z.twa + 4;
+            const uint32_t rtw = reload ? z.B : z.tw;
+            const uint32_t c = (rtw >> (8 * (uint32_t)(rq & 3))) & 0xFFu;
+            const uint32_t rkind = rec_kind(A), first = A.x & 0xFFFFFFu;
+            const uint32_t jr = rec_kid_index(A, c);
+            const bool rend = z.dd >= z.av;
+            const bool rnext = !rend && rkind == RT_REC_KIDS_K && jr != ((A.x >> 24) & 63u);
+            const bool rwide = !rend && rkind == RT_REC_WIDE_K;
+            // TS_WIDE: A is the quarter of the wide entry holding byte key
+            const uint32_t wnode = wide_child(A, key);
+            const bool wnext = wnode != ~0u;
+
+            // next state
+            uint32_t nst = TS_EMPTY, ans = 0;
+            bool fin = false;
+            if (st == TS_ITEM) nst = TS_KEY;
+            if (st == TS_KEY) nst = s2 ? TS_PROBE1 : TS_EMPTY;
+            if (st == TS_PROBE1 || st == TS_PROBE2) {
+                nst = pwalk ? TS_REC : pslot2 ? TS_PROBE2 : TS_EMPTY;
+                fin = match && !pwalk;
+                ans = pans;
+            }
+            if (st == TS_REC) {
+                nst = rnext ? TS_REC : rwide ? TS_WIDE : TS_EMPTY;
+                fin = !rnext && !rwide;
+                ans = A.y;
+            }
+            if (st == TS_WIDE) {
+                nst = wnext ? TS_REC : TS_EMPTY;
+                fin = !wnext;
+                ans = A.w;
+            }
+            if (fin) {
+                cnt += (uint32_t)(ans != 0u) - (z.pos >> 31);
+                if (OUTW) put_id<OUTW>(out, (int64_t)off, ans);
+            }
+            // registers of the next state
+            if (st == TS_ITEM) {
+                z.pos = z.B;
+                z.av = io + ctx + 1 > 1024u ? 1024u : io + ctx + 1;
+            }
+            if (st == TS_KEY) {
+                z.key = k32;
+                z.tw = lo;  // the dword before i's
+                z.twa = (int32_t)(off & ~3u) - 4;
+            }
+            if (st == TS_PROBE1 || st == TS_PROBE2) {
+                z.node = pnode;
+                z.dd = kind3 == 2 ? 3u : 4u;
+            }
+            if (st == TS_REC) {
+                z.tw = rtw;
+                z.twa = reload ? (rq & ~3) : z.twa;
+                z.node = rnext ? first + jr : first;
+                z.dd += rnext ? 1u : 0u;
+                z.key = rwide ? c : z.key;
+            }
+            if (st == TS_WIDE) {
+                z.node = wnode;
+                z.dd += 1;
+            }
+            z.st = nst;
+            // addresses of the next state's loads
+            const uint32_t noff = z.pos & RT_POSMASK, nob = noff & ~15u;
+            const int32_t nq = (int32_t)noff - (int32_t)z.dd;
+            const bool nreload = z.dd < z.av && (nq < z.twa || nq >= z.twa + 4);
+            const tu32x4* pa = dummy4;
+            const uint32_t* pb = dummy1;
+            if (nst == TS_KEY) {
+                pa = reinterpret_cast<const tu32x4*>(tb + nob);
+                if (nob + ctx >= 1) pb = reinterpret_cast<const uint32_t*>(tb + nob) - 1;
+            }
+            if (nst == TS_PROBE1) pa = T3 + rt_slot1(z.key >> 8, t.t3h_bits);
+            if (nst == TS_PROBE2) pa = T3 + rt_slot2(z.key >> 8, t.t3h_bits);
+            if (nst == TS_REC) {
+                pa = RC + z.node;
+                if (nreload) pb = reinterpret_cast<const uint32_t*>(tb + (nq & ~3));
+            }
+            if (nst == TS_WIDE) pa = WD + (size_t)A.z * 4 + (c >> 6);  // the quarter holding byte c
+            z.pa = pa;
+            z.pb = pb;
+        });
+    }
+}
+
+template <int V, int OUTW>
 __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
                                                              int64_t pos0, int64_t n, void* __restrict__ out,
                                                              unsigned long long* __restrict__ count, RtDev t) {
@@ -218,13 +442,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     }
     __syncthreads();
 
-    // VT >= 20: variant VT - 20 with each wave on a contiguous span of chunks
-    constexpr int V = VT >= 20 ? VT - 20 : VT;
-    constexpr bool kSpan = VT >= 20;
-    // ablation phase switches (V = 0: all on)
-    constexpr bool kFilter = V == 0 || V >= 5;
-    constexpr bool kPush = kFilter && V != 11;
-    constexpr bool kRounds = kPush && V != 12 && V != 13;
+    // ablation phase switches (V = 0: all on; V = 3: product kernel with
+    // the plain one-walk-per-lane tail, a cross-check of rt_tail; V = 6:
+    // no deep walks at all, timing only)
+    constexpr bool kFilter = V == 0 || V >= 3;
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -233,9 +454,6 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     uint32_t* qpos = s_qpos[wid];
     uint32_t cnt = 0;   // per lane
     uint32_t scnt = 0;  // per wave (scalar): the chunks' nonzero placeholders
-    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t tA = 0, tB = 0;
-    if (V == 9) tA = stamp();
     // chunk c is "fast" (main loop) when all of it is in range and it starts
     // >= 2 bytes into the stream: chunks [c_lo, c_hi)
     const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
@@ -244,17 +462,13 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // this wave's chunks: cbeg, cbeg + cstep, ... below cend
     const int64_t gw = (int64_t)blockIdx.x * RT_WAVES + wid;
     const int64_t nw = (int64_t)gridDim.x * RT_WAVES;
-    int64_t cbeg, cend, cstep;
-    if (kSpan) {
-        const int64_t per = (c_hi - c_lo + nw - 1) / nw;
-        cbeg = c_lo + gw * per;
-        cend = cbeg + per < c_hi ? cbeg + per : c_hi;
-        cstep = 1;
-    } else {
-        cbeg = c_lo + gw;
-        cend = c_hi;
-        cstep = nw;
-    }
+    const int64_t cbeg = c_lo + gw, cend = c_hi, cstep = nw;
+    // this wave's spill region: the candidates of chunks whose queue room
+    // ran out (dense deep matches), walked after the chunk loop (rt_tail).
+    // At most one item per position of the wave's chunks, which is the
+    // region's size.
+    uint32_t* const sp = t.spill + gw * t.spill_stride;
+    uint32_t sn = 0;  // wave-uniform
     // out-of-range prefetches read this instead (any >= 1 KiB of table)
     const uint8_t* dummy = reinterpret_cast<const uint8_t*>(t.filt) + 4;
     using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
@@ -265,23 +479,25 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // qkey = record | depth << 23); qpos = position - pos0 (30 bits) |
     // probe-slot2 << 30.  The match count is settled when a candidate
     // resolves or turns into record steps (its placeholder is the t12 entry
-    // of its key, recomputed then).  A candidate probes t3h
-    // slot1 only: the key there resolves it, and so does an empty slot1
-    // (cuckoo entries are only ever swapped, so a key whose slot1 is empty
-    // is absent); only a slot1 holding another key sends it to slot2 next
-    // round.  So a round has one scattered load per item (the other three
-    // are scattered only over record steps, a few lanes).
-    // Rounds are software-pipelined: issue() loads one set per item (a t3h
-    // slot, or the 48-B record + the next stream byte) into the
+    // of its key, recomputed then).  A candidate probes t3h slot1 only: the
+    // key there resolves it, and so does an empty slot1 (cuckoo entries are
+    // only ever swapped, so a key whose slot1 is empty is absent); only a
+    // slot1 holding another key sends it to slot2 next round.  A record step
+    // (qkey = record | depth << 23) loads the 16-B record and the next
+    // stream byte; at a wide record (more than RT_REC_INLINE children) the
+    // item turns into a wide step (qpos bit 30; qkey = entry | byte << 14 |
+    // depth << 22) that loads the one 16-B quarter of the entry deciding
+    // the byte.  So a round has one scattered load per item.
+    // Rounds are software-pipelined: issue() loads one set per item into the
     // round registers, and consume() uses them in the next chunk iteration,
     // so the load latency hides behind a chunk's store, push and LDS work.
-    // Unfinished items go back to the queue for the next round.
-    // The chunk loop is unrolled by two with fixed A/B text windows, so no
-    // loaded register is ever copied (a copy would wait for the load), and
-    // every round issues the same four loads
-    // (idle lanes read a harmless address), so the vmcnt the compiler
-    // computes is static: waiting for a chunk's bytes or for a round never
-    // waits for the younger rounds, stores and prefetches.
+    // Unfinished items go back to the queue for the next round.  The chunk
+    // loop is unrolled by two with fixed A/B text windows, so no loaded
+    // register is ever copied (a copy would wait for the load), and every
+    // round issues the same two loads (idle lanes read a harmless address),
+    // so the vmcnt the compiler computes is static: waiting for a chunk's
+    // bytes or for a round never waits for the younger rounds, stores and
+    // prefetches.
     // Ordering: items of chunk k are issued after chunk k's placeholder
     // store, and vmcnt retires in order, so a round's results imply the
     // stores of its items are complete at L2 before any patch overwrites one.
@@ -290,12 +506,12 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         uint32_t keep;  // items that may survive the round (wave-uniform): ring room they hold
         uint32_t fk, fp, tc;
         uint32_t skip;  // stage 2 rejected the item: its answer is the placeholder
-        u32x4 L0, L1, L2;
+        u32x4 L0;
     };
     // The queue is a ring of RT_QCAP items per wave: head qh, count qn.  A
-    // round takes all queued items once RT_ROUND are queued
-    // (idle chunks issue an empty round: same four loads, harmless
-    // addresses), so every round runs all 64 lanes.
+    // round takes all queued items once RT_ROUND are queued (idle chunks
+    // issue an empty round: same loads, harmless addresses), so every round
+    // runs all 64 lanes.
     uint32_t qh = 0, qn = 0;  // wave-uniform
     auto issue = [&](Round& r, uint32_t take) __attribute__((always_inline)) {
         __builtin_amdgcn_wave_barrier();
@@ -315,23 +531,16 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         r.keep = (uint32_t)__popcll(__ballot(act && !skip));
         const uint32_t k = r.fk >> 8;
         const uint32_t node = r.fk & 0x7FFFFFu, d = r.fk >> 23;
+        const bool wide = deep && (r.fp & RT_SLOT2);  // record step at a wide node: its quarter
         const int64_t i = pos0 + (int64_t)(r.fp & RT_POSMASK);
-        const u32x4* R = reinterpret_cast<const u32x4*>(t.rec) + (size_t)node * 3;
         const u32x4* T = reinterpret_cast<const u32x4*>(t.t3h);
         const u32x4* F = reinterpret_cast<const u32x4*>(t.filt);  // a harmless line
         const uint32_t slot = (r.fp & RT_SLOT2) ? rt_slot2(k, t.t3h_bits) : rt_slot1(k, t.t3h_bits);
-        const u32x4* a0 = deep ? R : (skip ? F : T + slot);
-        const u32x4* a1 = deep ? R + 1 : F;
-        const u32x4* a2 = deep ? R + 2 : F;
-        const uint8_t* a3 = (deep && (int64_t)d <= i - stream_start) ? text + (i - d) : dummy;
-        if (V == 5) {  // ablation: every round load hits one line (results wrong)
-            a0 = a1 = a2 = F;
-            a3 = dummy;
-        }
+        const u32x4* W = reinterpret_cast<const u32x4*>(t.wide) + (size_t)(r.fk & 0x3FFFu) * 4 + ((r.fk >> 20) & 3u);
+        const u32x4* a0 = wide ? W : deep ? reinterpret_cast<const u32x4*>(t.rec) + node : ((act && !skip) ? T + slot : F);
+        const uint8_t* a1 = (deep && !wide && (int64_t)d <= i - stream_start) ? text + (i - d) : dummy;
         r.L0 = *a0;
-        r.L1 = *a1;
-        r.L2 = *a2;
-        r.tc = *a3;
+        r.tc = *a1;
         r.n = take;
         qh += take;
         qn -= take;
@@ -340,11 +549,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         // Nothing computed from the round may be hoisted above this point
         // (the compiler otherwise speculates it up to the loads and waits).
         // (Fenced copies: the round's own registers are never redefined.)
-        u32x4 L0 = r.L0, L1 = r.L1, L2 = r.L2;
+        u32x4 L0 = r.L0;
         uint32_t tc = r.tc, fk = r.fk, fp = r.fp;
-        asm volatile("" : "+v"(L0), "+v"(L1), "+v"(L2), "+v"(tc), "+v"(fk), "+v"(fp)::"memory");
-        if (V == 9) { const uint64_t u = stamp(); ph[2] += u - tB; tB = u; }
-        bool again = false;
+        asm volatile("" : "+v"(L0), "+v"(tc), "+v"(fk), "+v"(fp)::"memory");
+        bool again = false, wstep = false;
         uint32_t nk = 0, np = 0;
         if ((uint32_t)lane < r.n && !r.skip) {
             const int64_t i = pos0 + (int64_t)(fp & RT_POSMASK);
@@ -382,27 +590,42 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                         d = 3;
                     }
                 }
+            } else if (fp & RT_SLOT2) {
+                // wide step: L0 = the quarter of the node's wide entry
+                // holding byte c; fk = entry | c << 14 | depth << 22
+                const uint32_t ch = wide_child(L0, (fk >> 14) & 0xFFu);
+                d = (fk >> 22) + 1;
+                v = L0.w;
+                if (ch != ~0u) {
+                    node = ch;
+                    again = true;
+                }
             } else {
+                // record step: {kind | count | first, best, child bytes}
                 d = fk >> 23;
-                v = L2.y;  // {base, best, prefix lo, prefix hi}
+                const u32x4 R = L0;
+                v = R.y;
                 if ((int64_t)d < avail) {
-                    const uint32_t w = tc >> 5, bit = tc & 31u;
-                    // bit-test select tree (an equality chain becomes a
-                    // dynamic extract, which lowers through scratch)
-                    const uint32_t s0 = (w & 1) ? L0.y : L0.x, s1 = (w & 1) ? L0.w : L0.z;
-                    const uint32_t s2 = (w & 1) ? L1.y : L1.x, s3 = (w & 1) ? L1.w : L1.z;
-                    const uint32_t s4 = (w & 2) ? s1 : s0, s5 = (w & 2) ? s3 : s2;
-                    const uint32_t word = (w & 4) ? s5 : s4;
-                    if ((word >> bit) & 1u) {
-                        const uint32_t pre = ((w < 4 ? L2.z : L2.w) >> (8 * (w & 3))) & 0xFFu;
-                        node = L2.x + pre + __popc(word & ((1u << bit) - 1u));
-                        ++d;
+                    const uint32_t kind = rec_kind(R);
+                    if (kind == RT_REC_KIDS_K) {
+                        const uint32_t j = rec_kid_index(R, tc);
+                        if (j != ((R.x >> 24) & 63u)) {
+                            node = (R.x & 0xFFFFFFu) + j;
+                            ++d;
+                            again = true;
+                        }
+                    } else if (kind == RT_REC_WIDE_K) {
+                        wstep = true;  // next round: the quarter of its entry holding tc
                         again = true;
+                        node = R.z | (tc << 14);
                     }
                 }
             }
             if (reprobe) {
                 nk = fk;
+                np = fp | RT_SLOT2;
+            } else if (wstep) {
+                nk = node | (d << 22);
                 np = fp | RT_SLOT2;
             } else if (again) {
                 nk = node | (d << 23);
@@ -410,7 +633,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 if (!(fp >> 31)) cnt -= (uint32_t)(ph0 != 0u);  // the placeholder leaves the count
             } else {
                 cnt += (uint32_t)(v != 0u) - ((fp >> 31) ? 0u : (uint32_t)(ph0 != 0u));
-                if (OUTW && V != 6 && v != ph0) put_id<OUTW>(out, i - pos0, v);
+                if (OUTW && v != ph0) put_id<OUTW>(out, i - pos0, v);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -454,11 +677,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     uint32_t xa[4], xb[4], pa, pb;
     int64_t ch = cbeg;
     // One chunk: depth<=2 answers from LDS, filter, the previous chunk's
-    // round consumed and a new one issued, the store,
-    // the push of this chunk's candidates, the prefetch two chunks ahead.
+    // round consumed and a new one issued, the store, the push of this
+    // chunk's candidates, the prefetch two chunks ahead.
     auto chunk = [&](uint32_t (&xr)[4], uint32_t& xp, int64_t c) __attribute__((always_inline)) {
         const int64_t pc = pos0 + c * RT_CHUNK;
-        if (V == 9) { tB = stamp(); ph[6] += 1; }
         // 8-byte windows {previous dword, own dword}: wave_shr:1 hands each
         // lane its left neighbour's dword; lane 0 keeps `old`: the previous
         // group's lane-63 dword (wave_ror:1 of that group), or for group 0
@@ -477,20 +699,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         uint32_t res[16];
         uint32_t cm = 0;  // bit j: position j goes past depth 2
 #pragma unroll
-        for (int j = 0; j < 16; ++j) res[j] = (V >= 2 && V <= 4) ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
-        if (V == 3) {  // streaming + latency-like delay (the wave yields its SIMD)
-#pragma unroll 1
-            for (int k = 0; k < 40; ++k) __builtin_amdgcn_s_sleep(2);
-        }
-        if (V == 4) {  // streaming + ~500 dependent VALU per chunk
-            uint32_t z = res[0];
-#pragma unroll 1
-            for (int k = 0; k < 125; ++k) {
-                z = z * 3u + 1u;
-                z ^= z >> 7;
-            }
-            res[0] ^= (z == 0x12345u);
-        }
+        for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
         if (kFilter) {
             uint32_t fw[16];
 #pragma unroll
@@ -507,30 +716,17 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             res[j] &= 0x7FFFu;
             scnt += (uint32_t)__popcll(__ballot(res[j] != 0u));
         }
-        if (V == 9) { const uint64_t u = stamp(); ph[0] += u - tB; tB = u; }
-        if (V == 11) asm volatile("" ::"v"(cm));  // keeps the filter live
-        if (kRounds) {
-            if (rr.n) consume(rr);                      // the round issued last chunk
-            if (V == 9) { const uint64_t u = stamp(); ph[3] += u - tB; tB = u; }
+        if (kFilter) {
+            if (rr.n) consume(rr);                // the round issued last chunk
             issue(rr, qn >= RT_ROUND ? qn : 0u);  // items of earlier chunks (stores issued)
-            if (V == 9) { const uint64_t u = stamp(); ph[5] += u - tB; tB = u; }
         }
         // store the chunk: depth<=2 answers, queued positions patched later
-        if (OUTW == 4 && V != 10) {
+        if (OUTW == 4) {
             u32x4* o = reinterpret_cast<u32x4*>(reinterpret_cast<uint32_t*>(out) + (pc - pos0));
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 u32x4 v = {res[4 * s], res[4 * s + 1], res[4 * s + 2], res[4 * s + 3]};
                 __builtin_nontemporal_store(v, o + 64 * s + lane);
-            }
-        }
-        if (OUTW == 4 && V == 10) {  // ablation: sc1 (L2-dropping) chunk stores
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<uint32_t*>(out) + (pc - pos0), 0, 0x7fffffff, 0x00020000);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                u32x4 v = {res[4 * s], res[4 * s + 1], res[4 * s + 2], res[4 * s + 3]};
-                __builtin_amdgcn_raw_buffer_store_b128(v, rs, (1024 * s + 16 * lane), 0, 16);
             }
         }
         if (OUTW == 2) {  // 512 contiguous bytes per store instruction
@@ -542,20 +738,20 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             }
         }
         asm volatile("" ::: "memory");  // the store stays ahead of any later probe
-        if (V == 9) { const uint64_t u = stamp(); ph[4] += u - tB; tB = u; }
-        if (kPush) {
+        if (kFilter) {
             // lane count c = popc(cm); exclusive wave prefix by a DPP scan;
             // items written by a loop over the lane's own set bits
             const uint32_t c = __popc(cm);
             const uint32_t incl = wave_scan_incl(c);
             const uint32_t base = incl - c;
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-            if (V == 13) asm volatile("" ::"v"(base), "s"(total));  // ablation: scan only
-            if (V != 13 && total <= RT_QCAP - qn - rr.keep) {
-                // common case: the whole chunk fits; straight-line per-item
-                // body (the window's bytes i-3..i by one 64-bit shift)
-                uint32_t mm = cm, slot = qh + qn + base;
-                const uint32_t pbase = (uint32_t)(pc - pos0) + 4 * lane;
+            uint32_t mm = cm;
+            const uint32_t pbase = (uint32_t)(pc - pos0) + 4 * lane;
+            if (total <= RT_QCAP - qn - rr.keep) {
+                // the whole chunk fits the ring (the in-flight round's
+                // possible survivors keep their room); the window's bytes
+                // i-3..i by one 64-bit shift
+                uint32_t slot = qh + qn + base;
                 while (mm) {
                     const uint32_t j = __builtin_ctz(mm);
                     mm &= mm - 1;
@@ -568,45 +764,23 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                     ++slot;
                 }
                 qn += total;
-            } else
-            for (uint32_t done = 0; V != 13;) {  // wave-uniform
-                // the in-flight round's possible survivors keep their room
-                const uint32_t room = RT_QCAP - qn - rr.keep;
-                uint32_t mm = cm, rank = base;
-                while (mm) {  // per lane: its own candidates, in position order
+            } else {
+                // ring full (dense matches): the chunk's candidates go to
+                // the spill region, walked after the chunk loop, with
+                // whether their placeholder (t12 of the key) is nonzero
+                uint32_t k = sn + base;
+                while (mm) {
                     const uint32_t j = __builtin_ctz(mm);
                     mm &= mm - 1;
-                    if (rank >= done && rank - done < room) {
-                        const uint32_t slot = (qh + qn + rank - done) & (RT_QCAP - 1);
-                        const uint32_t sg = j >> 2, b = j & 3;
-                        // bit-test select tree (no dynamic register index)
-                        const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
-                        const u32x2 w = (sg & 2) ? w23 : w01;
-                        // text[i-3..i] = window bytes 1+b .. 4+b (alignbit uses
-                        // the shift mod 32, so b = 3 is the high word itself)
-                        qkey[slot] = b == 3 ? w.y : __builtin_amdgcn_alignbit(w.y, w.x, 8 * (1 + b));
-                        qpos[slot] = (uint32_t)(pc - pos0) + 256 * sg + 4 * lane + b;
-                    }
-                    ++rank;
+                    const uint32_t sg = j >> 2, b = j & 3;
+                    const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
+                    const u32x2 w = (sg & 2) ? w23 : w01;
+                    const uint32_t key = (uint32_t)((((uint64_t)w.y << 32) | w.x) >> (8 * (2 + b))) & 0xFFFFFFu;
+                    const uint32_t ph = (s_t[key >> 8] & 0x7FFFu) != 0u;
+                    sp[k++] = (pbase + 256 * sg + b) | (ph << 31);
                 }
-                const uint32_t took = total - done < room ? total - done : room;
-                qn += took;
-                done += took;
-                if (done == total) break;
-                // ring full (dense matches): resolve synchronously in
-                // separate registers; these waits cover this chunk's stores
-                if (rr.n) {
-                    consume(rr);
-                } else {
-                    Round rs;
-                    issue(rs, qn);
-                    consume(rs);
-                }
-            }
-            if (V == 9) { const uint64_t u = stamp(); ph[1] += u - tB; tB = u; }
-            if (V == 12) {  // ablation: drop the queue (no rounds)
-                qh += qn;
-                qn = 0;
+                // (readfirstlane: keeps the count scalar across the branch)
+                sn = __builtin_amdgcn_readfirstlane(sn + total);
             }
         }
         fetch(xr, xp, c + 2 * cstep);
@@ -615,10 +789,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // store, prefetch; round, store, prefetch) so the compiler's vmcnt is the
     // steady-state one.
     Round r0;
-    if (kRounds) issue(r0, 0);
+    if (kFilter) issue(r0, 0);
     stand_in_store();
     fetch(xa, pa, ch);
-    if (kRounds) issue(rr, 0);
+    if (kFilter) issue(rr, 0);
     stand_in_store();
     fetch(xb, pb, ch + cstep);
     for (;;) {  // wave-uniform
@@ -628,19 +802,33 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         chunk(xb, pb, ch + cstep);
         ch += 2 * cstep;
     }
-    if (kRounds) {
+    if (kFilter) {
         if (rr.n) consume(rr);
         while (qn) {  // wave-uniform; every round advances each item
             Round rs;
             issue(rs, qn);
             consume(rs);
         }
-    }
-    if (V == 9) {
-        ph[7] = stamp() - tA;
-        if (lane == 0 && count)
-            for (int k = 0; k < 8; ++k) atomicAdd(count + k, (unsigned long long)ph[k]);
-        return;
+        // every placeholder and spill store of this wave complete before
+        // its walks patch or read them
+        __builtin_amdgcn_s_waitcnt(0);
+        if (V == 6) {
+            cnt += sn;  // timing only: the chunk loop without the deep walks
+        } else if (V == 3) {
+            for (uint32_t k = lane; k < sn; k += 64) {
+                const uint32_t item = sp[k];
+                const int64_t i = pos0 + (int64_t)(item & RT_POSMASK);
+                const uint32_t v = rt_one(text, s_t, t, i, stream_start);
+                cnt += (uint32_t)(v != 0u) - (item >> 31);
+                if (OUTW) put_id<OUTW>(out, (int64_t)(item & RT_POSMASK), v);
+            }
+        } else if (V == 4) {
+            rt_tail<OUTW, 2>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+        } else if (V == 5) {
+            rt_tail<OUTW, 8>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+        } else {
+            rt_tail<OUTW>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+        }
     }
     // the (at most two) chunks that touch the stream start or the tail: one
     // position per thread of the last workgroup (a chunk is 1024 positions),
@@ -844,9 +1032,28 @@ __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint6
 
 }  // namespace
 
+// Workgroups of an RT launch over n positions (persistent: one 1024-lane
+// workgroup per CU, LDS-bound) and the spill items its waves may need.
+static int64_t rt_blocks(int64_t n, int num_cu) {
+    const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
+    const int64_t blocks = (nchunks + RT_WAVES - 1) / RT_WAVES;
+    return blocks > num_cu ? num_cu : (blocks < 1 ? 1 : blocks);
+}
+static int64_t rt_spill_stride(int64_t n, int64_t blocks) {
+    const int64_t nw = blocks * RT_WAVES;
+    return ((n / RT_CHUNK + nw - 1) / nw) * RT_CHUNK;  // a wave's main-loop chunks, one item per position
+}
+
+int64_t pm_rt_spill_items(int64_t n, int num_cu) {
+    constexpr int64_t PIECE = (int64_t)RT_POSMASK + 1;
+    const int64_t m = n > PIECE ? PIECE : n;
+    const int64_t blocks = rt_blocks(m, num_cu);
+    return blocks * RT_WAVES * rt_spill_stride(m, blocks);
+}
+
 static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
-                                 void* out, int outw, unsigned long long* count, const RtDev& t, int num_cu,
-                                 hipStream_t s, int blocks_override) {
+                                 void* out, int outw, unsigned long long* count, const RtDev& t0, int num_cu,
+                                 hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (!out) outw = 0;
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
@@ -856,16 +1063,15 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         for (int64_t off = 0; off < n; off += PIECE) {
             const int64_t m = n - off < PIECE ? n - off : PIECE;
             void* o = outw ? reinterpret_cast<uint8_t*>(out) + off * outw : nullptr;
-            hipError_t e = launch_rt_impl(variant, text, stream_start, pos0 + off, m, o, outw, count, t, num_cu, s,
-                                          blocks_override);
+            hipError_t e = launch_rt_impl(variant, text, stream_start, pos0 + off, m, o, outw, count, t0, num_cu, s);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
-    int64_t blocks = (nchunks + RT_WAVES - 1) / RT_WAVES;
-    if (blocks > num_cu) blocks = num_cu;  // persistent: one 1024-lane workgroup per CU (LDS-bound)
-    if (blocks_override > 0) blocks = blocks_override;
+    const int64_t blocks = rt_blocks(n, num_cu);
+    RtDev t = t0;
+    t.spill_stride = rt_spill_stride(n, blocks);
+    if (blocks * RT_WAVES * t.spill_stride > t.spill_cap) return hipErrorInvalidValue;  // caller sizes it (pm_rt_spill_items)
     const dim3 g((unsigned)blocks), b(RT_THREADS);
 #define RT_LAUNCH(VV)                                                                                             \
     do {                                                                                                          \
@@ -883,13 +1089,6 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 4: RT_LAUNCH(4); break;
         case 5: RT_LAUNCH(5); break;
         case 6: RT_LAUNCH(6); break;
-        case 10: RT_LAUNCH(10); break;
-        case 11: RT_LAUNCH(11); break;
-        case 12: RT_LAUNCH(12); break;
-        case 13: RT_LAUNCH(13); break;
-        case 9: RT_LAUNCH(9); break;
-        case 20: RT_LAUNCH(20); break;
-        case 22: RT_LAUNCH(22); break;
         default: RT_LAUNCH(0);
     }
 #undef RT_LAUNCH
@@ -898,13 +1097,13 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
 
 hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                         unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s) {
-    return launch_rt_impl(0, text, stream_start, pos0, n, out, outw, count, t, num_cu, s, 0);
+    return launch_rt_impl(0, text, stream_start, pos0, n, out, outw, count, t, num_cu, s);
 }
 
 hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
                                 void* out, int outw, unsigned long long* count, const RtDev& t, int num_cu,
-                                hipStream_t s, int blocks_override) {
-    return launch_rt_impl(variant, text, stream_start, pos0, n, out, outw, count, t, num_cu, s, blocks_override);
+                                hipStream_t s) {
+    return launch_rt_impl(variant, text, stream_start, pos0, n, out, outw, count, t, num_cu, s);
 }
 
 // DFA launch shape: lanes (segments in flight) per CU; pm_dfa_set_shape

@@ -66,6 +66,8 @@ struct PipeSlot {
     size_t cap = 0;  // positions
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint32_t* spill = nullptr;  // RT deep-walk scratch of this slot's launches
+    int64_t spill_cap = 0;
     bool busy = false;
     size_t off = 0, m = 0;  // block = positions [off, off + m) of the call
 };
@@ -90,6 +92,8 @@ struct PmHip {
     bool cache_hit = false;
     std::vector<void*> allocs;
     size_t table_bytes = 0;
+    uint32_t* spill = nullptr;  // RT deep-walk scratch of scan_device launches
+    int64_t spill_cap = 0;
     // streaming: the carried history and a two-slot pipeline (scan_host)
     std::vector<uint8_t> hist;
     std::vector<pm_pattern_id_t> id_of_gid;  // [0] = PM_NULL_PATTERN_ID
@@ -128,8 +132,24 @@ void free_slot(PipeSlot& q) {
         (void)hipHostFree(q.h_stage);
         (void)hipHostFree(q.h_res);
     }
+    if (q.spill) (void)hipFree(q.spill);
     q.d_stage = nullptr;
+    q.spill = nullptr;
+    q.spill_cap = 0;
     q.cap = 0;
+}
+
+// The RT kernel's spill regions (pm_kernels.h): one u32 per position of a
+// launch, grown to the largest launch seen (scratch, not part of the
+// automaton's total_mem).
+void ensure_spill(PmHip* o, uint32_t*& buf, int64_t& cap, int64_t n) {
+    if (o->kind != KIND_RT) return;
+    const int64_t need = pm_rt_spill_items(n, o->num_cu);
+    if (need <= cap) return;
+    if (buf) PM_CHECK(hipFree(buf));
+    buf = nullptr;
+    PM_CHECK(hipMalloc(&buf, (size_t)need * sizeof(uint32_t)));
+    cap = need;
 }
 
 void ensure_slot(PmHip* o, PipeSlot& q, size_t positions) {
@@ -146,6 +166,7 @@ void ensure_slot(PmHip* o, PipeSlot& q, size_t positions) {
     PM_CHECK(hipMalloc(&q.d_res, cap * sizeof(uint32_t)));
     PM_CHECK(hipHostMalloc(&q.h_stage, stage_bytes, hipHostMallocDefault));
     PM_CHECK(hipHostMalloc(&q.h_res, cap * sizeof(uint32_t), hipHostMallocDefault));
+    ensure_spill(o, q.spill, q.spill_cap, (int64_t)cap);
     q.cap = cap;
 }
 
@@ -181,8 +202,13 @@ void par_range(size_t n, size_t grain, const F& f) {
 }
 
 hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
-                  unsigned long long* count, hipStream_t s) {
-    if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, o->rt, o->num_cu, s);
+                  unsigned long long* count, hipStream_t s, uint32_t* spill, int64_t spill_cap) {
+    if (o->kind == KIND_RT) {
+        RtDev t = o->rt;
+        t.spill = spill;
+        t.spill_cap = spill_cap;
+        return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
+    }
     return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
 }
 
@@ -240,7 +266,8 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         PM_CHECK(hipMemcpyAsync(q.d_stage + ctx, buf + done, m, hipMemcpyHostToDevice, q.stream));
         PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
         PM_CHECK(hipEventRecord(q.ev0, q.stream));
-        PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, 4, nullptr, q.stream));
+        PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, 4, nullptr, q.stream,
+                        q.spill, q.spill_cap));
         PM_CHECK(hipEventRecord(q.ev1, q.stream));
         PM_CHECK(hipMemcpyAsync(out_gid ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
                                 hipMemcpyDeviceToHost, q.stream));
@@ -318,7 +345,8 @@ void pm_hip_compile(void* obj) {
         o->rt.filt = (const uint32_t*)dalloc_copy(o, im.rt.filt.data(), im.rt.filt.size() * 4);
         o->rt.t3h = (const uint4*)dalloc_copy(o, im.rt.t3h.data(), im.rt.t3h.size() * 4);
         o->rt.t3h_bits = im.rt.t3h_bits;
-        o->rt.rec = (const uint32_t*)dalloc_copy(o, im.rt.rec.data(), im.rt.rec.size() * 4);
+        o->rt.rec = (const uint4*)dalloc_copy(o, im.rt.rec.data(), im.rt.rec.size() * 4);
+        o->rt.wide = (const uint4*)dalloc_copy(o, im.rt.wide.data(), im.rt.wide.size() * 4);
         const std::vector<uint8_t> zero(RT_SCRATCH_BYTES, 0);
         o->rt.scratch = (uint32_t*)dalloc_copy(o, zero.data(), zero.size());
     } else {
@@ -367,6 +395,7 @@ void pm_hip_free(void* obj) {
     PmHip* o = as(obj);
     (void)hipSetDevice(o->device);
     for (void* p : o->allocs) (void)hipFree(p);
+    if (o->spill) (void)hipFree(o->spill);
     for (PipeSlot& q : o->slot) {
         free_slot(q);
         if (q.ev0) (void)hipEventDestroy(q.ev0);
@@ -406,7 +435,11 @@ static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
         return -4;
     }
     hipError_t e = hipSetDevice(o->device);
-    if (e == hipSuccess) e = launch(o, d_text, stream_start, pos0, n, d_out, outw, d_count, (hipStream_t)hip_stream);
+    if (e == hipSuccess) {
+        ensure_spill(o, o->spill, o->spill_cap, n);
+        e = launch(o, d_text, stream_start, pos0, n, d_out, outw, d_count, (hipStream_t)hip_stream, o->spill,
+                   o->spill_cap);
+    }
     if (e != hipSuccess) {
         std::snprintf(g_err, sizeof(g_err), "launch: %s", hipGetErrorString(e));
         return -3;
@@ -473,11 +506,15 @@ uint32_t pm_hip_parent_gid(void* obj, uint32_t gid) {
 
 // Timing-only ablation launches of the RT kernel (bench_variants.py).
 int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out, int out_width,
-                              unsigned long long* d_count, void* hip_stream, int blocks) {
+                              unsigned long long* d_count, void* hip_stream) {
     PmHip* o = as(obj);
     if (o->kind != KIND_RT) return -1;
-    hipError_t e = pm_launch_rt_variant(variant, d_text, 0, 0, n, d_out, out_width, d_count, o->rt, o->num_cu,
-                                        (hipStream_t)hip_stream, blocks);
+    ensure_spill(o, o->spill, o->spill_cap, n);
+    RtDev t = o->rt;
+    t.spill = o->spill;
+    t.spill_cap = o->spill_cap;
+    hipError_t e = pm_launch_rt_variant(variant, d_text, 0, 0, n, d_out, out_width, d_count, t, o->num_cu,
+                                        (hipStream_t)hip_stream);
     return e == hipSuccess ? 0 : -3;
 }
 
@@ -558,6 +595,7 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
     if (s == "filt") return ret(h->rt.filt);
     if (s == "t3h") return ret(h->rt.t3h);
     if (s == "rec") return ret(h->rt.rec);
+    if (s == "wide") return ret(h->rt.wide);
     if (s == "next") return ret(h->dfa.next);
     if (s == "out") return ret(h->dfa.out);
     if (s == "index_of_gid") return ret(h->g.index_of_gid);

@@ -18,7 +18,6 @@ ap.add_argument("--bytes", type=int, default=1 << 30)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--stream", type=int, default=0, help="0 ascii, 1 bytes, 2 the shipped stream tiled")
 ap.add_argument("--variants", default="0,1,2")
-ap.add_argument("--blocks", default="0")
 ap.add_argument("--modes", default="dense,dense16,count")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
@@ -40,40 +39,22 @@ else:
     lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, 1, args.stream, s.cuda_stream)
 out = torch.empty(n, dtype=torch.int32, device="cuda")
 cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
-variants = [(int(v), mode, int(b)) for v in args.variants.split(",") for mode in args.modes.split(",")
-            for b in args.blocks.split(",")]
+variants = [(int(v), mode) for v in args.variants.split(",") for mode in args.modes.split(",")]
 times = {k: [] for k in variants}
 for r in range(args.rounds + 1):
-    for (v, mode, b) in variants:
+    for (v, mode) in variants:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         rc = lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, out.data_ptr() if mode != "count" else None,
-                                           WIDTH[mode], cnt.data_ptr(), s.cuda_stream, b)
+                                           WIDTH[mode], cnt.data_ptr(), s.cuda_stream)
         assert rc == 0
         e1.record(s)
         torch.cuda.synchronize()
         if r:
-            times[(v, mode, b)].append(e0.elapsed_time(e1))
+            times[(v, mode)].append(e0.elapsed_time(e1))
 res = {}
-if "9" in args.variants.split(","):
-    for mode in args.modes.split(","):
-        cnt.zero_()
-        lib.pm_hip_debug_scan_variant(m.obj, 9, text.data_ptr(), n, out.data_ptr() if mode != "count" else None,
-                                      WIDTH[mode], cnt.data_ptr(), s.cuda_stream, 0)
-        torch.cuda.synchronize()
-        c = [int(x) for x in cnt.tolist()]
-        names = ["lds_filter", "push", "round_wait", "consume", "store", "issue", "chunks", "total"]
-        res[f"v9-stamps-{mode}"] = {k: (c[i] / c[6] if i != 6 else c[i]) for i, k in enumerate(names)}
-for v in ():
-    if str(v) in args.variants.split(","):
-        cnt.zero_()
-        lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, None, 0, cnt.data_ptr(), s.cuda_stream, 0)
-        torch.cuda.synchronize()
-        res[f"v{v}-counter"] = {"value": int(cnt.item()), "per_position": int(cnt.item()) / n}
-for (v, mode, b), t in times.items():
-    if v == 9:
-        continue
+for (v, mode), t in times.items():
     ms = statistics.median(t)
-    res[f"v{v}-{mode}-b{b}"] = {"ms": round(ms, 4), "min": round(min(t), 4), "GBps_stream": round(n / ms / 1e6, 1),
-                                "alg_GBps": round(n * (1 + WIDTH[mode]) / ms / 1e6, 1)}
+    res[f"v{v}-{mode}"] = {"ms": round(ms, 4), "min": round(min(t), 4), "GBps_stream": round(n / ms / 1e6, 1),
+                           "alg_GBps": round(n * (1 + WIDTH[mode]) / ms / 1e6, 1)}
 print(json.dumps(res, indent=1))

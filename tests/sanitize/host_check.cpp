@@ -53,15 +53,29 @@ uint32_t rt_deep(const RtImage& im, const std::vector<uint8_t>& text, uint32_t n
                  int64_t d) {
     for (;;) {
         const size_t R = (size_t)node * RT_REC_WORDS;
-        const uint32_t base = im.rec.at(R + 8), best = im.rec.at(R + 9);
+        const uint32_t x = im.rec.at(R), best = im.rec.at(R + 1);
         if (d >= avail) return best;
+        const uint32_t kind = x >> 30, cnt = (x >> 24) & 63u, first = x & 0xFFFFFFu;
         const uint32_t c = text.at(i - d);
-        const uint32_t w = c >> 5, bit = c & 31u;
-        const uint32_t word = im.rec.at(R + w);
-        if (!((word >> bit) & 1u)) return best;
-        const uint32_t pre = (im.rec.at(R + 10 + (w >> 2)) >> (8 * (w & 3))) & 0xFFu;
-        node = base + pre + (uint32_t)__builtin_popcount(word & ((1u << bit) - 1u));
-        CHECK(node < im.nrec, "record %u of %u", node, im.nrec);
+        if (kind == RT_REC_LEAF) return best;
+        uint32_t next = 0;
+        if (kind == RT_REC_KIDS) {
+            uint32_t j = 0;
+            while (j < cnt && ((im.rec.at(R + 2 + j / 4) >> (8 * (j & 3))) & 0xFFu) != c) ++j;
+            if (j == cnt) return best;
+            next = first + j;
+        } else {
+            CHECK(kind == RT_REC_WIDE, "record kind %u", kind);
+            const size_t Q = (size_t)im.rec.at(R + 2) * RT_WIDE_WORDS + 4 * (c >> 6);
+            const uint32_t w = (c >> 5) & 1u, word = im.wide.at(Q + w), bit = c & 31u;
+            CHECK(im.wide.at(Q + 3) == best, "wide best %u vs %u", im.wide.at(Q + 3), best);
+            if (!((word >> bit) & 1u)) return best;
+            next = im.wide.at(Q + 2) + (w ? (uint32_t)__builtin_popcount(im.wide.at(Q)) : 0u) +
+                   (uint32_t)__builtin_popcount(word & ((1u << bit) - 1u));
+            CHECK(im.wide.at(Q + 2) >= first, "wide index %u below first %u", im.wide.at(Q + 2), first);
+        }
+        CHECK(next > node && next < im.nrec, "record %u -> %u of %u", node, next, im.nrec);
+        node = next;
         ++d;
     }
 }
@@ -182,7 +196,7 @@ int main(int argc, char** argv) {
     CHECK(hit, "rt: second build missed the cache");
     CHECK(rt1.rt.fits && rt2.rt.fits, "rt image does not fit");
     CHECK(rt1.rt.t12 == rt2.rt.t12 && rt1.rt.filt == rt2.rt.filt && rt1.rt.t3h == rt2.rt.t3h &&
-              rt1.rt.rec == rt2.rt.rec && rt1.rt.t3h_bits == rt2.rt.t3h_bits && rt1.rt.nrec == rt2.rt.nrec,
+              rt1.rt.rec == rt2.rt.rec && rt1.rt.wide == rt2.rt.wide && rt1.rt.t3h_bits == rt2.rt.t3h_bits && rt1.rt.nrec == rt2.rt.nrec,
           "rt: cached image differs");
     PmImages df1 = pm_build_images_cached(fd.pats, g, 2, cache, &hit);
     CHECK(!hit, "dfa: first build hit the cache");

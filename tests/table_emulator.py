@@ -90,17 +90,29 @@ def t3h_lookup(t3h, bits, key24):
     return None
 
 
-def rec_walk(rec, text, p, avail, node, d):
+def rec_walk(rec, wide, text, p, avail, node, d):
+    """16-B node records (pm_flatten.h): leaf / up to 8 inline children /
+    wide (4 quarters {word 2q, word 2q+1, first child index, best})."""
     while True:
-        R = rec[node]
+        x, best, z, w = (int(v) for v in rec[node])
         if d >= avail:
-            return int(R[9])
+            return best
+        kind, cnt, first = x >> 30, (x >> 24) & 63, x & 0xFFFFFF
         c = int(text[p - d])
-        w, bit = c >> 5, c & 31
-        if not (int(R[w]) >> bit) & 1:
-            return int(R[9])
-        pre = (int(R[10 + (w >> 2)]) >> (8 * (w & 3))) & 0xFF
-        node = int(R[8]) + pre + bin(int(R[w]) & ((1 << bit) - 1)).count("1")
+        if kind == 0:
+            return best
+        if kind == 1:
+            kids = [((z | (w << 32)) >> (8 * j)) & 0xFF for j in range(cnt)]
+            if c not in kids:
+                return best
+            node = first + kids.index(c)
+        else:
+            Q = [int(v) for v in wide[z][4 * (c >> 6):4 * (c >> 6) + 4]]  # {word 2q, word 2q+1, index, best}
+            w = (c >> 5) & 1
+            word = Q[w]
+            if not (word >> (c & 31)) & 1:
+                return Q[3]
+            node = Q[2] + (bin(Q[0]).count("1") if w else 0) + bin(word & ((1 << (c & 31)) - 1)).count("1")
         d += 1
 
 
@@ -110,7 +122,8 @@ def rt_scan(img, text, stream_start=0, use_filter=True):
     filt = img.array("filt")
     t3h = img.array("t3h")
     bits = int(len(t3h) // 4).bit_length() - 1
-    rec = img.array("rec").reshape(-1, 12)
+    rec = img.array("rec").reshape(-1, 4)
+    wide = img.array("wide").reshape(-1, 16)
     text = np.asarray(text, dtype=np.uint8)
     n = len(text)
     i = np.arange(n, dtype=np.int64)
@@ -140,13 +153,13 @@ def rt_scan(img, text, stream_start=0, use_filter=True):
             if c3 not in kids:
                 out[p] = e[1]
             elif nch > 1:
-                out[p] = rec_walk(rec, text, p, avail[p], e[3] + kids.index(c3), 4)
+                out[p] = rec_walk(rec, wide, text, p, avail[p], e[3] + kids.index(c3), 4)
             elif not e[3] & 0x80000000:
                 out[p] = e[3]
             else:
-                out[p] = rec_walk(rec, text, p, avail[p], e[3] & 0x7FFFFFFF, 4)
+                out[p] = rec_walk(rec, wide, text, p, avail[p], e[3] & 0x7FFFFFFF, 4)
         else:
-            out[p] = rec_walk(rec, text, p, avail[p], e[3] & 0x7FFFFFFF, 3)
+            out[p] = rec_walk(rec, wide, text, p, avail[p], e[3] & 0x7FFFFFFF, 3)
     return out
 
 

@@ -126,7 +126,7 @@ def test_compiled_image_cache(tmp_path):
     truncated or foreign file is rebuilt; another dictionary gets its own file."""
     d = pm.Dictionary(dict_paths("et"))
     pats = d.patterns()
-    names = {pm.KIND_RT: ["t12", "filt", "t3h", "rec", "parent", "depth"], pm.KIND_AC: ["next", "out", "parent", "depth"]}
+    names = {pm.KIND_RT: ["t12", "filt", "t3h", "rec", "wide", "parent", "depth"], pm.KIND_AC: ["next", "out", "parent", "depth"]}
     for kind, arrays in names.items():
         a = FlatImage(pats, kind, tmp_path)
         assert not a.cache_hit
@@ -165,8 +165,8 @@ def test_compiled_image_cache_rejects_a_damaged_filter(tmp_path):
     a = FlatImage(pats, pm.KIND_RT, tmp_path)
     (f,) = tmp_path.glob(f"pm-{pm.KIND_RT}-*.img")
     raw = bytearray(f.read_bytes())
-    # header 24 B; sections: 16-B header + data (scal 7 u32, t12 u16[65792], filt)
-    off = 24 + 16 + 28 + 16 + 2 * 65792 + 16
+    # header 24 B; sections: 16-B header + data (scal 8 u32, t12 u16[65792], filt)
+    off = 24 + 16 + 32 + 16 + 2 * 65792 + 16
     filt = np.frombuffer(bytes(raw[off:off + 4 * 4096]), np.uint32)
     assert np.array_equal(filt, a.array("filt")[:4096])
     w = int(np.nonzero(filt)[0][0])
