@@ -10,9 +10,10 @@
 
 namespace {
 
-// A byte trie in BFS order: node 0 is the root, the children of a node are
-// contiguous ids [cstart, cstart+ccount) sorted by edge byte, and all nodes
-// of depth d precede all nodes of depth d+1.
+// A numbered byte trie: node 0 is the root, the children of a node are
+// contiguous ids [cstart, cstart+ccount) sorted by edge byte, a parent's id
+// is below its children's, and (build_trie) the first levels are in BFS
+// order.
 struct BfsTrie {
     uint32_t n = 0;
     std::vector<uint32_t> cstart, ccount, parent, gid, depth;
@@ -29,7 +30,14 @@ struct BfsTrie {
     }
 };
 
-BfsTrie build_trie(const std::vector<std::string>& pats, const PmGidMap& g, bool reversed) {
+// dfs_depth: nodes of depth <= dfs_depth are numbered breadth-first (all
+// of depth d before any of depth d+1); deeper ones get "children blocks in
+// depth-first order": visiting a node allocates its children's contiguous
+// block, then visits them first to last.  A unary chain's nodes are then
+// consecutive ids, so a walk down it reads consecutive 16-B records (8 to a
+// cache line) instead of one line per step.
+BfsTrie build_trie(const std::vector<std::string>& pats, const PmGidMap& g, bool reversed,
+                   uint32_t dfs_depth = UINT32_MAX) {
     // creation-order trie with a hash map of edges
     std::unordered_map<uint64_t, uint32_t> edge;
     size_t total = 0;
@@ -64,7 +72,8 @@ BfsTrie build_trie(const std::vector<std::string>& pats, const PmGidMap& g, bool
     std::vector<uint32_t> kstart(n + 1, 0);
     for (uint64_t x : kids) kstart[(x >> 40) + 1]++;
     for (uint32_t v = 0; v < n; ++v) kstart[v + 1] += kstart[v];
-    // BFS renumbering
+    // renumbering: a node's fields are set when it is expanded (its
+    // children block allocated)
     BfsTrie t;
     t.n = n;
     t.cstart.assign(n, 0);
@@ -73,21 +82,36 @@ BfsTrie build_trie(const std::vector<std::string>& pats, const PmGidMap& g, bool
     t.gid.assign(n, 0);
     t.depth.assign(n, 0);
     t.label.assign(n, 0);
-    std::vector<uint32_t> order;  // BFS id -> creation id
+    std::vector<uint32_t> order;  // new id -> creation id
     order.reserve(n);
     order.push_back(0);
-    for (size_t h = 0; h < order.size(); ++h) {
-        uint32_t old = order[h];
-        uint32_t v = (uint32_t)h;
+    auto expand = [&](uint32_t v) {
+        const uint32_t old = order[v];
         t.gid[v] = gid[old];
         t.cstart[v] = (uint32_t)order.size();
         t.ccount[v] = kstart[old + 1] - kstart[old];
         for (uint32_t k = kstart[old]; k < kstart[old + 1]; ++k) {
-            uint32_t nv = (uint32_t)order.size();
+            const uint32_t nv = (uint32_t)order.size();
             t.parent[nv] = v;
             t.label[nv] = (uint8_t)((kids[k] >> 32) & 0xFF);
             t.depth[nv] = t.depth[v] + 1;
             order.push_back((uint32_t)(kids[k] & 0xFFFFFFFFu));
+        }
+    };
+    std::vector<uint32_t> deep;  // nodes at dfs_depth, in breadth-first order
+    for (size_t h = 0; h < order.size(); ++h) {
+        const uint32_t v = (uint32_t)h;
+        if (t.depth[v] < dfs_depth) expand(v);
+        else deep.push_back(v);
+    }
+    std::vector<uint32_t> stack;
+    for (uint32_t r : deep) {
+        stack.push_back(r);
+        while (!stack.empty()) {
+            const uint32_t v = stack.back();
+            stack.pop_back();
+            expand(v);
+            for (uint32_t k = t.ccount[v]; k-- > 0;) stack.push_back(t.cstart[v] + k);  // first child on top
         }
     }
     return t;
@@ -157,7 +181,7 @@ PmGidMap pm_assign_gids(const std::vector<std::string>& pats) {
 
 RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
     RtImage im;
-    BfsTrie t = build_trie(pats, g, /*reversed=*/true);
+    BfsTrie t = build_trie(pats, g, /*reversed=*/true, /*dfs_depth=*/3);
     im.nodes = t.n;
     // best pattern on the path root..v (deepest pattern node, inclusive)
     std::vector<uint32_t> best(t.n, 0);
@@ -296,7 +320,7 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
 PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap& g) {
     // In the trie of the reversed patterns the nodes above a pattern's node
     // are its suffixes, so its parent is the deepest pattern strictly above.
-    BfsTrie t = build_trie(pats, g, /*reversed=*/true);
+    BfsTrie t = build_trie(pats, g, /*reversed=*/true, /*dfs_depth=*/3);
     std::vector<uint32_t> best(t.n, 0);
     PmParents r;
     r.parent.assign(g.index_of_gid.size(), 0);
@@ -348,7 +372,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 6;                     // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 7;                     // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);

@@ -12,14 +12,14 @@ struct RtDev {
     const uint4* rec;      // nrec 16-B node records
     const uint4* wide;     // 4 quarters {word 2q, word 2q+1, child index, best} per wide node
     uint32_t* scratch;     // RT_SCRATCH_BYTES the kernel may overwrite (stand-in stores)
-    uint32_t* spill;       // spill_cap u32: per-wave regions of deep-walk items (scratch)
-    int64_t spill_cap;
-    int64_t spill_stride;  // set per launch
+    uint32_t* spill;       // spill_cap 8-B items: per-wave regions of overflow candidates (scratch)
+    int64_t spill_cap;     // items
+    int64_t spill_stride;  // items per wave region, set per launch
     uint32_t t3h_bits;
 };
 
-// Spill items (u32) an RT launch over n positions needs in RtDev::spill: one
-// per position of each wave's chunks.  Launches of any n reuse one buffer of
+// Spill items (8 B each) an RT launch over n positions needs in
+// RtDev::spill: one per position of each wave's chunks.  Launches of any n reuse one buffer of
 // this size for n' <= n.
 int64_t pm_rt_spill_items(int64_t n, int num_cu);
 

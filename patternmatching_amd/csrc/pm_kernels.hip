@@ -210,15 +210,6 @@ __device__ __forceinline__ void put_id(void* out, int64_t k, uint32_t v) {
     if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[k] = (uint16_t)v;
 }
 
-// Deep walks of one wave's spilled positions (items sp[0, sn): position -
-// pos0 | placeholder-nonzero << 31), after its chunk loop.  Every lane keeps
-// RT_TAIL_SLOTS walks in lock step, each one load per iteration (its
-// item, its 16-B text block, a t3h slot, a record, a wide quarter), so a wave
-// has 64 * RT_TAIL_SLOTS dependent chains in flight.  Each walk ends by
-// writing its answer and settling the count against its placeholder.
-constexpr int RT_TAIL_SLOTS = 4;
-enum : uint32_t { TS_EMPTY = 0, TS_ITEM, TS_KEY, TS_PROBE1, TS_PROBE2, TS_REC, TS_WIDE };
-
 // f(integral_constant<int, 0>) .. f(integral_constant<int, N-1>): a loop the
 // compiler sees fully unrolled with constant indices (per-slot state stays
 // in registers)
@@ -230,182 +221,224 @@ __device__ __forceinline__ void unroll_for(F&& f) {
     }
 }
 
+using tu32x2 = __attribute__((ext_vector_type(2))) unsigned int;
 using tu32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+
+// The deep work of one wave's spilled candidates, after its chunk loop.
+// Items sp[0, sn) are {text[i-3..i], position - pos0 | placeholder-nonzero
+// << 31} (8 B).  Two phases, each uniform code:
+//  1. probe: batches of 64 * RT_PROBE_G items, one per lane per group:
+//     stage 2, the t3h slot1 probe (slot2 where slot1 holds another key).
+//     A position that resolves there is written; one whose walk goes on
+//     is compacted in place into a walk entry {record, position - pos0 |
+//     (depth == 4) << 30 | placeholder-nonzero << 31}.
+//  2. walk: RT_TAIL_SLOTS walks per lane in lock step, refilled from the
+//     walk entries; each iteration issues one record (or wide quarter)
+//     load and, when the next byte is not in the lane's 8 cached text
+//     bytes, the aligned 8 bytes holding it.  A wave keeps 64 *
+//     RT_TAIL_SLOTS dependent chains in flight with a short branch-free
+//     body per step.
+// Each position ends by writing its answer and settling the count against
+// its placeholder.  (Measured and not kept: fetching the walk's first text
+// bytes in phase 1, with 16-B entries, and writing the walk answers in
+// position order from the entries afterwards -- both slower.)
+constexpr int RT_PROBE_G = 4;
+constexpr int RT_TAIL_SLOTS = 4;
+constexpr uint32_t RT_D4 = 1u << 30;  // walk entry: starts at depth 4 (else 3)
+enum : uint32_t { TS_EMPTY = 0, TS_ENTRY, TS_REC, TS_WIDE };
+
 // One in-flight walk.  Offsets are u32 from pos0; pa / pb are the next
-// iteration's load addresses (set when the state changes), so issuing is
-// two loads per slot whatever the state.
+// iteration's load addresses, so issuing is two loads per slot whatever the
+// state.
 struct TailSlot {
     uint32_t st;          // TS_*
     uint32_t pos;         // position - pos0 | placeholder-nonzero << 31
     uint32_t av;          // bytes at or before the position, capped at 1024
-    uint32_t key;         // text[i-3..i] (LE); TS_WIDE: the byte c
     uint32_t node, dd;    // record, depth (bytes consumed)
-    uint32_t tw;          // cached text dword
-    int32_t twa;          // its offset (dword-aligned, may precede pos0)
+    uint32_t c;           // TS_WIDE: the byte being decided; TS_ENTRY: entry parity
+    uint32_t tlo, thi;    // cached text bytes [twa, twa + 8)
+    int32_t twa;          // (4-aligned, may precede pos0)
     const tu32x4* pa;
-    const uint32_t* pb;
+    const tu32x2* pb;
     tu32x4 A;             // this iteration's 16-B load
-    uint32_t B;           // this iteration's dword load
+    tu32x2 B;             // this iteration's 8-B load
 };
 
-template <int OUTW, int SLOTS = RT_TAIL_SLOTS>
+template <int OUTW, bool kProbeOnly = false, int SLOTS = RT_TAIL_SLOTS>
 __device__ __forceinline__ void rt_tail(const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0,
                                         void* __restrict__ out, const RtDev& t, const uint32_t* s_f2,
-                                        const uint32_t* sp, uint32_t sn, int lane, uint32_t& cnt) {
+                                        uint32_t* sp, uint32_t sn, int lane, uint32_t& cnt) {
     const uint8_t* const tb = text + pos0;  // offsets are from pos0; pos0 % 16 == 0
     const int64_t ctx64 = pos0 - stream_start;  // context bytes before pos0
     const uint32_t ctx = ctx64 > 1024 ? 1024u : (uint32_t)ctx64;
     const tu32x4* const dummy4 = reinterpret_cast<const tu32x4*>(t.filt);
-    const uint32_t* const dummy1 = t.filt;
+    const tu32x2* const dummy2 = reinterpret_cast<const tu32x2*>(t.filt);
     const tu32x4* const T3 = reinterpret_cast<const tu32x4*>(t.t3h);
     const tu32x4* const RC = reinterpret_cast<const tu32x4*>(t.rec);
     const tu32x4* const WD = reinterpret_cast<const tu32x4*>(t.wide);
+    tu32x2* const items = reinterpret_cast<tu32x2*>(sp);
+
+    // ---- phase 1: probes ------------------------------------------------
+    uint32_t nwalk = 0;  // wave-uniform
+    for (uint32_t base = 0; base < sn; base += 64 * RT_PROBE_G) {
+        tu32x2 it[RT_PROBE_G];
+        tu32x4 e[RT_PROBE_G];
+        bool act[RT_PROBE_G];
+        unroll_for<0, RT_PROBE_G>([&](auto g) __attribute__((always_inline)) {
+            const uint32_t idx = base + 64 * g + lane;
+            it[g] = idx < sn ? items[idx] : tu32x2{0u, 0u};
+            act[g] = idx < sn && rt_stage2_hit(rt_stage2_load(s_f2, it[g].x)) != 0u;
+        });
+        unroll_for<0, RT_PROBE_G>([&](auto g) __attribute__((always_inline)) {
+            e[g] = act[g] ? T3[rt_slot1(it[g].x >> 8, t.t3h_bits)] : *dummy4;
+        });
+        bool need2[RT_PROBE_G];
+        bool any2 = false;
+        unroll_for<0, RT_PROBE_G>([&](auto g) __attribute__((always_inline)) {
+            const uint32_t want = T3H_VALID | (it[g].x >> 8);
+            need2[g] = act[g] && (e[g].x & 0x1FFFFFFu) != want && (e[g].x & T3H_VALID);
+            any2 |= need2[g];
+        });
+        if (__ballot(any2)) {  // wave-uniform
+            unroll_for<0, RT_PROBE_G>([&](auto g) __attribute__((always_inline)) {
+                if (need2[g]) e[g] = T3[rt_slot2(it[g].x >> 8, t.t3h_bits)];
+            });
+        }
+        unroll_for<0, RT_PROBE_G>([&](auto g) __attribute__((always_inline)) {
+            const tu32x4 E = e[g];
+            const uint32_t key = it[g].x, pw = it[g].y, off = pw & RT_POSMASK;
+            const bool match = act[g] && (E.x & 0x1FFFFFFu) == (T3H_VALID | (key >> 8));
+            const uint32_t kind = E.x >> 25, nch = E.z >> 24, c3 = key & 0xFFu;
+            const uint32_t j = c3 == (E.z & 0xFFu) ? 0u : c3 == ((E.z >> 8) & 0xFFu) ? 1u
+                             : c3 == ((E.z >> 16) & 0xFFu) ? 2u : 3u;
+            const bool deep4 = off + ctx >= 3;  // avail >= 4
+            const bool inl = kind == 1 && j < nch && nch == 1 && !(E.w & CONT32);
+            const bool walk = match && deep4 && ((kind == 1 && j < nch && !inl) || kind == 2);
+            const uint32_t node = (kind == 2 || nch == 1) ? E.w & 0x7FFFFFFFu : E.w + j;
+            const uint32_t ans = (deep4 && inl) ? E.w : E.y;
+            if (match && !walk) {
+                cnt += (uint32_t)(ans != 0u) - (pw >> 31);
+                if (OUTW) put_id<OUTW>(out, (int64_t)off, ans);
+            }
+            // walk entries compacted in place: entry nwalk + k never passes
+            // an item not yet read (every item of this batch is in registers)
+            const uint64_t m = __ballot(walk);
+            if (walk) items[nwalk + wave_prefix(m)] = tu32x2{node, (pw & ~RT_D4) | (kind == 1 ? RT_D4 : 0u)};
+            nwalk += (uint32_t)__popcll(m);
+        });
+    }
+    if (!nwalk || kProbeOnly) return;
+    // the walk entries are stored (vmcnt 0) and this CU's L1 dropped
+    // (phase 1 read the same lines before overwriting them) before they are
+    // read
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+
+    // ---- phase 2: walks -------------------------------------------------
     TailSlot S[SLOTS];
     unroll_for<0, SLOTS>([&](auto I) __attribute__((always_inline)) {
         TailSlot& z = S[I];
         z.st = TS_EMPTY;
-        z.pos = z.av = z.key = z.node = z.dd = z.tw = z.B = 0;
+        z.pos = z.av = z.node = z.dd = z.c = z.tlo = z.thi = 0;
         z.twa = 0;
         z.pa = dummy4;
-        z.pb = dummy1;
+        z.pb = dummy2;
         z.A = tu32x4{0u, 0u, 0u, 0u};
+        z.B = tu32x2{0u, 0u};
     });
-    uint32_t nxt = 0;  // wave-uniform: next unclaimed item
+    uint32_t nxt = 0;  // wave-uniform: next unclaimed walk entry
     for (;;) {
-        // refill empty slots with the next items, in item order across lanes
         bool busy = false;
         unroll_for<0, SLOTS>([&](auto I) __attribute__((always_inline)) {
             TailSlot& z = S[I];
             const bool need = z.st == TS_EMPTY;
             const uint64_t m = __ballot(need);
             const uint32_t idx = nxt + wave_prefix(m);
-            if (need && idx < sn) {
-                z.st = TS_ITEM;
-                z.pa = dummy4;
-                z.pb = sp + idx;
+            if (need && idx < nwalk) {
+                z.st = TS_ENTRY;
+                z.c = idx & 1u;  // the entry's half of the 16-B load
+                z.pa = reinterpret_cast<const tu32x4*>(items + (idx & ~1u));
+                z.pb = dummy2;
             }
             nxt += (uint32_t)__popcll(m);
-            if (nxt > sn) nxt = sn;
+            if (nxt > nwalk) nxt = nwalk;
             busy |= z.st != TS_EMPTY;
         });
         if (!__ballot(busy)) break;  // wave-uniform
-        // issue: every slot's two loads in flight together
         unroll_for<0, SLOTS>([&](auto I) __attribute__((always_inline)) {
             TailSlot& z = S[I];
             z.A = *z.pa;
             z.B = *z.pb;
         });
-        // resolve, branch-free: every state's outcome is computed and the
-        // slot's own selected (divergent branches per state cost more than
-        // the arithmetic: exec-mask bookkeeping and register merges)
+        // branch-free step: each state's outcome is computed and the slot's
+        // own selected (divergent branches cost more: exec-mask bookkeeping
+        // and register merges)
         unroll_for<0, SLOTS>([&](auto I) __attribute__((always_inline)) {
             TailSlot& z = S[I];
             const uint32_t st = z.st;
             const tu32x4 A = z.A;
+            // TS_ENTRY: {record, position | d4 | ph}
+            const uint32_t en = z.c ? A.z : A.x, ep = z.c ? A.w : A.y;
+            // TS_REC: A is the record; B the aligned 8 text bytes holding
+            // text[i-d] when they were not cached
             const uint32_t off = z.pos & RT_POSMASK;
-            // TS_ITEM: B is the item
-            const uint32_t io = z.B & RT_POSMASK, iob = io & ~15u;
-            // TS_KEY: text[i-3..i] from the 20-byte window {dword before
-            // the block, the block}.  Bit-test select tree: an equality chain
-            // over the vector's components compiles to a dynamic extract,
-            // measured wrong for q = 3 on gfx950.
-            const uint32_t q = (off >> 2) & 3u, b = off & 3u;
-            const uint32_t h01 = (q & 1) ? A.y : A.x, h23 = (q & 1) ? A.w : A.z;
-            const uint32_t l01 = (q & 1) ? A.x : z.B, l23 = (q & 1) ? A.z : A.y;
-            const uint32_t hi = (q & 2) ? h23 : h01, lo = (q & 2) ? l23 : l01;
-            const uint32_t k32 = b == 3 ? hi : __builtin_amdgcn_alignbit(hi, lo, 8 * (b + 1));
-            const bool s2 = rt_stage2_hit(rt_stage2_load(s_f2, k32)) != 0u;
-            // TS_PROBE1/2: A is the t3h slot of key >> 8
-            const uint32_t key = z.key;
-            const bool match = (A.x & 0x1FFFFFFu) == (T3H_VALID | (key >> 8));
-            const uint32_t kind3 = A.x >> 25, nch = A.z >> 24, c3 = key & 0xFFu;
-            const uint32_t j3 = c3 == (A.z & 0xFFu) ? 0u : c3 == ((A.z >> 8) & 0xFFu) ? 1u
-                              : c3 == ((A.z >> 16) & 0xFFu) ? 2u : 3u;
-            const bool deep4 = z.av >= 4;
-            const bool inl = kind3 == 1 && j3 < nch && nch == 1 && !(A.w & CONT32);  // the child's answer inline
-            const bool pwalk = match && deep4 && ((kind3 == 1 && j3 < nch && !inl) || kind3 == 2);
-            const uint32_t pnode = (kind3 == 2 || nch == 1) ? A.w & 0x7FFFFFFFu : A.w + j3;
-            const uint32_t pans = (match && deep4 && inl) ? A.w : A.y;
-            const bool pslot2 = !match && (A.x & T3H_VALID) && st == TS_PROBE1;
-            // TS_REC: A is the record, B the text dword when reloaded
             const int32_t rq = (int32_t)off - (int32_t)z.dd;
-            const bool reload = rq < z.twa || rq >= z.twa + 4;
-            const uint32_t rtw = reload ? z.B : z.tw;
-            const uint32_t c = (rtw >> (8 * (uint32_t)(rq & 3))) & 0xFFu;
+            const bool reload = rq < z.twa || rq >= z.twa + 8;
+            const uint32_t rlo = reload ? z.B.x : z.tlo, rhi = reload ? z.B.y : z.thi;
+            const int32_t rta = reload ? (rq & ~7) : z.twa;
+            const uint32_t ro = (uint32_t)(rq - rta);
+            const uint32_t c = ((ro & 4 ? rhi : rlo) >> (8 * (ro & 3))) & 0xFFu;
             const uint32_t rkind = rec_kind(A), first = A.x & 0xFFFFFFu;
             const uint32_t jr = rec_kid_index(A, c);
             const bool rend = z.dd >= z.av;
             const bool rnext = !rend && rkind == RT_REC_KIDS_K && jr != ((A.x >> 24) & 63u);
             const bool rwide = !rend && rkind == RT_REC_WIDE_K;
-            // TS_WIDE: A is the quarter of the wide entry holding byte key
-            const uint32_t wnode = wide_child(A, key);
+            // TS_WIDE: A is the quarter of the wide entry holding byte c
+            const uint32_t wnode = wide_child(A, z.c);
             const bool wnext = wnode != ~0u;
 
-            // next state
-            uint32_t nst = TS_EMPTY, ans = 0;
+            uint32_t nst = TS_EMPTY;
             bool fin = false;
-            if (st == TS_ITEM) nst = TS_KEY;
-            if (st == TS_KEY) nst = s2 ? TS_PROBE1 : TS_EMPTY;
-            if (st == TS_PROBE1 || st == TS_PROBE2) {
-                nst = pwalk ? TS_REC : pslot2 ? TS_PROBE2 : TS_EMPTY;
-                fin = match && !pwalk;
-                ans = pans;
+            uint32_t ans = A.w;  // TS_WIDE: the node's best
+            if (st == TS_ENTRY) {
+                nst = TS_REC;
+                z.node = en;
+                z.dd = (ep & RT_D4) ? 4u : 3u;
+                z.pos = ep & ~RT_D4;
+                const uint32_t o = ep & RT_POSMASK;
+                z.av = o + ctx + 1 > 1024u ? 1024u : o + ctx + 1;
+                z.twa = INT32_MIN / 2;  // nothing cached
             }
             if (st == TS_REC) {
                 nst = rnext ? TS_REC : rwide ? TS_WIDE : TS_EMPTY;
                 fin = !rnext && !rwide;
                 ans = A.y;
+                z.tlo = rlo;
+                z.thi = rhi;
+                z.twa = rta;
+                z.node = first + jr;
+                z.dd += rnext ? 1u : 0u;
+                z.c = c;
             }
             if (st == TS_WIDE) {
                 nst = wnext ? TS_REC : TS_EMPTY;
                 fin = !wnext;
-                ans = A.w;
-            }
-            if (fin) {
-                cnt += (uint32_t)(ans != 0u) - (z.pos >> 31);
-                if (OUTW) put_id<OUTW>(out, (int64_t)off, ans);
-            }
-            // registers of the next state
-            if (st == TS_ITEM) {
-                z.pos = z.B;
-                z.av = io + ctx + 1 > 1024u ? 1024u : io + ctx + 1;
-            }
-            if (st == TS_KEY) {
-                z.key = k32;
-                z.tw = lo;  // the dword before i's
-                z.twa = (int32_t)(off & ~3u) - 4;
-            }
-            if (st == TS_PROBE1 || st == TS_PROBE2) {
-                z.node = pnode;
-                z.dd = kind3 == 2 ? 3u : 4u;
-            }
-            if (st == TS_REC) {
-                z.tw = rtw;
-                z.twa = reload ? (rq & ~3) : z.twa;
-                z.node = rnext ? first + jr : first;
-                z.dd += rnext ? 1u : 0u;
-                z.key = rwide ? c : z.key;
-            }
-            if (st == TS_WIDE) {
                 z.node = wnode;
                 z.dd += 1;
             }
-            z.st = nst;
-            // addresses of the next state's loads
-            const uint32_t noff = z.pos & RT_POSMASK, nob = noff & ~15u;
-            const int32_t nq = (int32_t)noff - (int32_t)z.dd;
-            const bool nreload = z.dd < z.av && (nq < z.twa || nq >= z.twa + 4);
-            const tu32x4* pa = dummy4;
-            const uint32_t* pb = dummy1;
-            if (nst == TS_KEY) {
-                pa = reinterpret_cast<const tu32x4*>(tb + nob);
-                if (nob + ctx >= 1) pb = reinterpret_cast<const uint32_t*>(tb + nob) - 1;
+            if (fin) {
+                cnt += (uint32_t)(ans != 0u) - (z.pos >> 31);
+                if (OUTW) put_id<OUTW>(out, (int64_t)(z.pos & RT_POSMASK), ans);
             }
-            if (nst == TS_PROBE1) pa = T3 + rt_slot1(z.key >> 8, t.t3h_bits);
-            if (nst == TS_PROBE2) pa = T3 + rt_slot2(z.key >> 8, t.t3h_bits);
+            z.st = nst;
+            // the next state's loads
+            const int32_t nq = (int32_t)(z.pos & RT_POSMASK) - (int32_t)z.dd;
+            const bool nreload = z.dd < z.av && (nq < z.twa || nq >= z.twa + 8);
+            const tu32x4* pa = dummy4;
+            const tu32x2* pb = dummy2;
             if (nst == TS_REC) {
                 pa = RC + z.node;
-                if (nreload) pb = reinterpret_cast<const uint32_t*>(tb + (nq & ~3));
+                if (nreload) pb = reinterpret_cast<const tu32x2*>(tb + (nq & ~7));
             }
             if (nst == TS_WIDE) pa = WD + (size_t)A.z * 4 + (c >> 6);  // the quarter holding byte c
             z.pa = pa;
@@ -444,7 +477,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
 
     // ablation phase switches (V = 0: all on; V = 3: product kernel with
     // the plain one-walk-per-lane tail, a cross-check of rt_tail; V = 6:
-    // no deep walks at all, timing only)
+    // no tail at all, V = 7: the tail's probe phase only; both timing only)
     constexpr bool kFilter = V == 0 || V >= 3;
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
@@ -464,10 +497,11 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     const int64_t nw = (int64_t)gridDim.x * RT_WAVES;
     const int64_t cbeg = c_lo + gw, cend = c_hi, cstep = nw;
     // this wave's spill region: the candidates of chunks whose queue room
-    // ran out (dense deep matches), walked after the chunk loop (rt_tail).
+    // ran out (dense deep matches), {text[i-3..i], position - pos0 |
+    // placeholder-nonzero << 31}, resolved after the chunk loop (rt_tail).
     // At most one item per position of the wave's chunks, which is the
     // region's size.
-    uint32_t* const sp = t.spill + gw * t.spill_stride;
+    uint32_t* const sp = t.spill + 2 * gw * t.spill_stride;  // 8-B items
     uint32_t sn = 0;  // wave-uniform
     // out-of-range prefetches read this instead (any >= 1 KiB of table)
     const uint8_t* dummy = reinterpret_cast<const uint8_t*>(t.filt) + 4;
@@ -765,22 +799,33 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 }
                 qn += total;
             } else {
-                // ring full (dense matches): the chunk's candidates go to
-                // the spill region, walked after the chunk loop, with
-                // whether their placeholder (t12 of the key) is nonzero
-                uint32_t k = sn + base;
+                // ring full (dense matches): the first `room` candidates
+                // (in rank order) fill the ring, the rest go to the spill
+                // region, walked after the chunk loop, with whether their
+                // placeholder (t12 of the key) is nonzero
+                const uint32_t room = RT_QCAP - qn - rr.keep;
+                uint32_t rank = base;
                 while (mm) {
                     const uint32_t j = __builtin_ctz(mm);
                     mm &= mm - 1;
                     const uint32_t sg = j >> 2, b = j & 3;
                     const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
                     const u32x2 w = (sg & 2) ? w23 : w01;
-                    const uint32_t key = (uint32_t)((((uint64_t)w.y << 32) | w.x) >> (8 * (2 + b))) & 0xFFFFFFu;
-                    const uint32_t ph = (s_t[key >> 8] & 0x7FFFu) != 0u;
-                    sp[k++] = (pbase + 256 * sg + b) | (ph << 31);
+                    const uint32_t q32 = (uint32_t)((((uint64_t)w.y << 32) | w.x) >> (8 * (1 + b)));
+                    const uint32_t p = pbase + 256 * sg + b;
+                    if (rank < room) {
+                        const uint32_t sl = (qh + qn + rank) & (RT_QCAP - 1);
+                        qkey[sl] = q32;
+                        qpos[sl] = p;
+                    } else {
+                        const uint32_t ph = (s_t[q32 >> 16] & 0x7FFFu) != 0u;
+                        reinterpret_cast<u32x2*>(sp)[sn + rank - room] = u32x2{q32, p | (ph << 31)};
+                    }
+                    ++rank;
                 }
-                // (readfirstlane: keeps the count scalar across the branch)
-                sn = __builtin_amdgcn_readfirstlane(sn + total);
+                // (readfirstlane: keeps the counts scalar across the branch)
+                sn = __builtin_amdgcn_readfirstlane(sn + total - room);
+                qn = __builtin_amdgcn_readfirstlane(qn + room);
             }
         }
         fetch(xr, xp, c + 2 * cstep);
@@ -816,16 +861,18 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             cnt += sn;  // timing only: the chunk loop without the deep walks
         } else if (V == 3) {
             for (uint32_t k = lane; k < sn; k += 64) {
-                const uint32_t item = sp[k];
+                const uint32_t item = sp[2 * k + 1];
                 const int64_t i = pos0 + (int64_t)(item & RT_POSMASK);
                 const uint32_t v = rt_one(text, s_t, t, i, stream_start);
                 cnt += (uint32_t)(v != 0u) - (item >> 31);
                 if (OUTW) put_id<OUTW>(out, (int64_t)(item & RT_POSMASK), v);
             }
+        } else if (V == 7) {
+            rt_tail<OUTW, true>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
         } else if (V == 4) {
-            rt_tail<OUTW, 2>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+            rt_tail<OUTW, false, 8>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
         } else if (V == 5) {
-            rt_tail<OUTW, 8>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+            rt_tail<OUTW, false, 6>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
         } else {
             rt_tail<OUTW>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
         }
@@ -1089,6 +1136,7 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 4: RT_LAUNCH(4); break;
         case 5: RT_LAUNCH(5); break;
         case 6: RT_LAUNCH(6); break;
+        case 7: RT_LAUNCH(7); break;
         default: RT_LAUNCH(0);
     }
 #undef RT_LAUNCH

@@ -139,8 +139,8 @@ void free_slot(PipeSlot& q) {
     q.cap = 0;
 }
 
-// The RT kernel's spill regions (pm_kernels.h): one u32 per position of a
-// launch, grown to the largest launch seen (scratch, not part of the
+// The RT kernel's spill regions (pm_kernels.h): one 8-B item per position
+// of a launch, grown to the largest launch seen (scratch, not part of the
 // automaton's total_mem).
 void ensure_spill(PmHip* o, uint32_t*& buf, int64_t& cap, int64_t n) {
     if (o->kind != KIND_RT) return;
@@ -148,7 +148,7 @@ void ensure_spill(PmHip* o, uint32_t*& buf, int64_t& cap, int64_t n) {
     if (need <= cap) return;
     if (buf) PM_CHECK(hipFree(buf));
     buf = nullptr;
-    PM_CHECK(hipMalloc(&buf, (size_t)need * sizeof(uint32_t)));
+    PM_CHECK(hipMalloc(&buf, (size_t)need * 2 * sizeof(uint32_t)));  // 8-B items
     cap = need;
 }
 
