@@ -8,7 +8,10 @@ timed region) through the HIP kernel, writing the dense per-position match
 ids (u32; the read_block contract).  Shards are independent streams (one per
 rank, distinct seeds): weak scaling, no data-path collective.  The only
 collective is the RCCL all-reduce of match counts and the max-over-ranks
-time.
+time.  --layout split instead cuts ONE logical stream of N x --bytes into
+rank shards (patternmatching_amd.shard.shard_plan: each rank generates its
+shard plus the max_len-1 bytes before it as context), so the all-reduced
+match count is that of the whole stream.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -46,6 +49,9 @@ def parse():
                    help="ascii / bytes: seeded synthetic (DESIGN.md §5); ship: the reference's shipped "
                         "dictionaries_generated.stream tiled to --bytes (adversarial: deep matches)")
     p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--layout", default="shards", choices=["shards", "split"],
+                   help="shards: an independent seeded stream per rank; split: one stream of N x --bytes "
+                        "cut into rank shards with max_len-1 bytes of context (ascii / bytes streams)")
     p.add_argument("--cpu-sample", type=int, default=256 << 20, help="bytes of the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--score", action="store_true",
@@ -135,14 +141,21 @@ def main():
     import torch.distributed as dist
     import patternmatching_amd as pm
 
-    torch.cuda.set_device(local)
+    # one GPU per rank; a rehearsal with more ranks than GPUs (gloo) shares them
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     # the RCCL path runs for world > 1; PM_BENCH_DIST=1 runs it at world 1 too
-    # (one-GPU rehearsal of the multi-GPU code: init, barriers, all-reduces)
+    # (one-GPU rehearsal of the multi-GPU code: init, barriers, all-reduces).
+    # PM_BENCH_BACKEND=gloo rehearses several ranks on one GPU.
     use_dist = world > 1 or os.environ.get("PM_BENCH_DIST") == "1"
+    backend = os.environ.get("PM_BENCH_BACKEND", "nccl")
     if use_dist:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     lib = pm.load()
-    lib.pm_hip_set_device(local)
+    lib.pm_hip_set_device(dev)
 
     d = pm.Dictionary([os.path.join(DATA, x) for x in DICTS[args.dict]])
     m = pm.HipMatcher(args.kernel)
@@ -151,15 +164,25 @@ def main():
 
     n = args.bytes
     stream = torch.cuda.current_stream()
-    text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     seed = args.seed + rank  # independent shard per rank
+    pos0 = 0  # context bytes before the rank's first position (split layout)
+    gen_off = 0
+    if args.layout == "split":
+        if args.stream == "ship":
+            raise SystemExit("--layout split needs a generated stream (ascii / bytes)")
+        from patternmatching_amd.shard import shard_plan
+        seed = args.seed  # one logical stream
+        sh = shard_plan(world * n, world, rank, lib.pm_hip_max_pattern_len(m.obj))
+        ctx_lo = sh.ctx_lo & ~15  # 16-aligned: the scan starts on an aligned position
+        pos0, n, gen_off = sh.lo - ctx_lo, sh.hi - sh.lo, ctx_lo
+    text = torch.empty(pos0 + n + 64, dtype=torch.uint8, device="cuda")
     if args.stream == "ship":
         import numpy as np
         ship = torch.from_numpy(np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8))
         reps = (n + 64 + ship.numel() - 1) // ship.numel()
         text.copy_(ship.to("cuda").repeat(reps)[: n + 64])
-    elif lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, seed, 0 if args.stream == "ascii" else 1,
-                                      stream.cuda_stream) != 0:
+    elif lib.pm_hip_gen_stream_device(text.data_ptr(), gen_off, pos0 + n + 64, seed,
+                                      0 if args.stream == "ascii" else 1, stream.cuda_stream) != 0:
         raise RuntimeError(lib.pm_hip_last_error().decode())
     width = WIDTH[args.mode]
     out = torch.empty(n, dtype={4: torch.int32, 2: torch.int16}[width], device="cuda") if width else None
@@ -167,7 +190,7 @@ def main():
     out_ptr = out.data_ptr() if out is not None else None
 
     def step():
-        m.scan_device(text.data_ptr(), 0, 0, n, out_ptr, count.data_ptr(), stream.cuda_stream, out_width=width or 4)
+        m.scan_device(text.data_ptr(), 0, pos0, n, out_ptr, count.data_ptr(), stream.cuda_stream, out_width=width or 4)
 
     for _ in range(args.warmup):
         step()
@@ -207,7 +230,7 @@ def main():
             ac.add_dictionary(d)
             ac.compile()
             ref = torch.empty(n, dtype=torch.int32, device="cuda")
-            ac.scan_device(text.data_ptr(), 0, 0, n, ref.data_ptr(), None, stream.cuda_stream)
+            ac.scan_device(text.data_ptr(), 0, pos0, n, ref.data_ptr(), None, stream.cuda_stream)
             sc.zero_()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -234,7 +257,7 @@ def main():
     total_matches = int(matches.item())
 
     if rank == 0:
-        total_bytes = world * n * args.steps
+        total_bytes = world * args.bytes * args.steps  # every rank scans --bytes positions
         value = total_bytes / elapsed / 1e9
         alg_per_pos = 1 + width  # 1 B read + the id written per position
         achieved = n * alg_per_pos / (kernel_ms * 1e-3) / 1e9
@@ -265,7 +288,9 @@ def main():
                 "stream_bytes_per_gpu": n,
                 "mode": args.mode,
                 "kernel": {"rt": "reverse-suffix-trie walk", "ac": "Aho-Corasick dense DFA"}[args.kernel],
-                "parallelism": f"independent stream shards x{world}",
+                "parallelism": (f"independent stream shards x{world}" if args.layout == "shards" else
+                                f"one {world * args.bytes} B stream split x{world} (max_len-1 B context per shard)"),
+                "layout": args.layout,
             },
             "matches_per_sec": round(total_matches / elapsed, 1),
             "matches_per_step": total_matches // max(1, args.steps),

@@ -2,7 +2,7 @@
 """Copy one gpu_round.sh session (gpurun_out/round_TAG) into profiles/:
 the bench lines, the rocprofv3 kernel stats of the default bench, the PMC
 traffic summary, the GPU test log, and profiles/traffic.json (which bench.py
-reads for roofline.traffic).  Usage: collect_round.py TAG [profiles subdir]."""
+reads for roofline.traffic).  Usage: collect_round.py TAG [round, e.g. r02]."""
 import json
 import os
 import shutil
@@ -10,24 +10,28 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
-dst = os.path.join(REPO, "profiles", sys.argv[2] if len(sys.argv) > 2 else "r01")
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
+dst = os.path.join(REPO, "profiles", rnd)
 src = os.path.join(REPO, "gpurun_out", f"round_{tag}")
 os.makedirs(dst, exist_ok=True)
 names = {"dense": "C3 snort 1 GiB dense_u32 (bench default, 16-core reference baseline)",
          "dense16": "snort 1 GiB dense_u16", "count": "snort 1 GiB count_only",
          "ac": "snort 1 GiB AC dense DFA (reliable instance), dense_u32",
          "c2_et64m": "C2 et 64 MiB dense_u32", "c5_merged4g": "C5 merged 4 GiB dense_u32",
-         "score": "snort 1 GiB dense_u32 + on-device accuracy scoring vs the AC instance (--score)"}
+         "score": "snort 1 GiB dense_u32 + on-device accuracy scoring vs the AC instance (--score)",
+         "ship": "snort, the shipped stream tiled to 1 GiB (deep matches), dense_u32",
+         "ship_count": "snort, the shipped stream tiled to 1 GiB, count_only",
+         "ship_ac": "snort, the shipped stream tiled to 1 GiB, AC dense DFA, dense_u32"}
 lines = {}
 for k, label in names.items():
     p = os.path.join(src, f"bench_{k}.json")
     if os.path.exists(p):
         lines[label] = json.loads(open(p).read().strip().splitlines()[-1])
 lines["_session"] = f"scripts/gpu_round.sh {tag}; one MI355X box, one call"
-json.dump(lines, open(os.path.join(dst, "bench_r01.json"), "w"), indent=1)
+json.dump(lines, open(os.path.join(dst, f"bench_{rnd}.json"), "w"), indent=1)
 shutil.copy(os.path.join(src, "prof", "bench_kernel_stats.csv"),
             os.path.join(dst, "rt_dense_snort_1GiB_kernel_stats.csv"))
-shutil.copy(os.path.join(src, "pytest_gpu.log"), os.path.join(dst, "pytest_gpu_r01.log"))
+shutil.copy(os.path.join(src, "pytest_gpu.log"), os.path.join(dst, f"pytest_gpu_{rnd}.log"))
 pmc = json.load(open(os.path.join(src, "pmc_summary.json")))
 json.dump(pmc, open(os.path.join(dst, "rt_dense_snort_1GiB_pmc_traffic.json"), "w"), indent=1)
 tr_path = os.path.join(REPO, "profiles", "traffic.json")
@@ -36,7 +40,9 @@ key = "snort-ascii-1073741824-dense-rt"
 rd = pmc["FETCH_SIZE"] * 1024
 wr = pmc["WRITE_SIZE"] * 1024
 tr[key].update({"read_bytes_raw": rd, "read_bytes_corrected": 2 * rd, "write_bytes": wr,
-                "traffic_bytes": 2 * rd + wr, "session": f"gpu_round.sh {tag}"})
+                "traffic_bytes": 2 * rd + wr, "session": f"gpu_round.sh {tag}",
+                "source": f"profiles/{rnd}/rt_dense_snort_1GiB_pmc_traffic.json (rocprofv3 --pmc, one counter per pass, "
+                          "median over dispatches of rt_scan_kernel; 1 dispatch per 1 GiB step)"})
 json.dump(tr, open(tr_path, "w"), indent=1)
 for label, d in lines.items():
     if not label.startswith("_"):

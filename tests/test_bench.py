@@ -18,7 +18,7 @@ def _bench_args(**kw):
     sys.path.insert(0, REPO)
     import bench
     a = dict(gpus=1, steps=1, warmup=0, dict="et", bytes=1 << 20, mode="dense", kernel="rt", stream="ascii", seed=1,
-             cpu_sample=1 << 20, no_cpu=False, score=False)
+             cpu_sample=1 << 20, no_cpu=False, score=False, layout="shards")
     a.update(kw)
     return bench, argparse.Namespace(**a)
 
@@ -84,3 +84,23 @@ def test_bench_shipped_stream_and_score():
     assert acc["success"] == acc["positions"] == 16 << 20
     assert acc["false_pos_rate"] == acc["false_neg_rate"] == acc["partial_rate"] == 0.0
     assert d["cpu_baseline"] is None
+
+
+@pytest.mark.gpu
+def test_bench_split_layout_two_ranks_match_one_stream():
+    """--layout split with 2 ranks (gloo rehearsal: both ranks on this GPU)
+    cuts one 32 MiB stream into shards with max_len-1 bytes of context; the
+    all-reduced match count equals one rank scanning the whole stream."""
+    whole = _run(["--mode", "count", "--bytes", str(32 << 20)])
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29541", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--bytes", str(16 << 20), "--steps", "2", "--warmup", "1", "--no-cpu", "--mode", "count",
+           "--layout", "split"]
+    e = dict(os.environ, PM_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=e, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    two = json.loads(lines[0])
+    assert two["n_gpus"] == 2 and two["config"]["layout"] == "split"
+    assert two["matches_per_step"] == whole["matches_per_step"]
