@@ -44,7 +44,8 @@ def parse():
     p.add_argument("--bytes", type=int, default=1 << 30, help="stream bytes per GPU")
     p.add_argument("--mode", default="dense", choices=list(WIDTH),
                    help="dense: u32 id per position; dense16: u16 id per position; count: match count only")
-    p.add_argument("--kernel", default="rt", choices=["rt", "ac"])
+    p.add_argument("--kernel", default="rt", choices=["rt", "ac", "auto"],
+                   help="rt: reverse-trie kernel; ac: the AC dense DFA; auto: both, picked per launch")
     p.add_argument("--stream", default="ascii", choices=["ascii", "bytes", "ship"],
                    help="ascii / bytes: seeded synthetic (DESIGN.md §5); ship: the reference's shipped "
                         "dictionaries_generated.stream tiled to --bytes (adversarial: deep matches)")
@@ -287,7 +288,9 @@ def main():
                 "dict": args.dict,
                 "stream_bytes_per_gpu": n,
                 "mode": args.mode,
-                "kernel": {"rt": "reverse-suffix-trie walk", "ac": "Aho-Corasick dense DFA"}[args.kernel],
+                "kernel": {"rt": "reverse-suffix-trie walk", "ac": "Aho-Corasick dense DFA",
+                           "auto": "auto: RT or AC-DFA per launch by the RT spill rate (last launch: %s)"
+                                   % {1: "RT", 2: "AC"}.get(m.kernel_last, "?")}[args.kernel],
                 "parallelism": (f"independent stream shards x{world}" if args.layout == "shards" else
                                 f"one {world * args.bytes} B stream split x{world} (max_len-1 B context per shard)"),
                 "layout": args.layout,

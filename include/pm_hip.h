@@ -44,6 +44,11 @@ extern "C" {
 /* ---- 1. plugin ABI (MpsElem members) ---------------------------------- */
 void* pm_hip_rt_create(void);
 void* pm_hip_ac_create(void);
+/* Both kernels; each launch picks one: the RT kernel, unless the last RT
+ * launch spilled more than 10% of its positions (dense deep matches), when
+ * the next 64 launches run the AC-DFA kernel.  reset()
+ * forgets the choice. */
+void* pm_hip_auto_create(void);
 void pm_hip_add_pattern(void* obj, char* pat, size_t len, pm_pattern_id_t id);
 void pm_hip_compile(void* obj);
 pm_pattern_id_t pm_hip_read_char(void* obj, char c);
@@ -54,6 +59,7 @@ void pm_hip_free(void* obj);
 
 void pm_mps_hip_rt_register(PmMpsElem* slot);
 void pm_mps_hip_ac_register(PmMpsElem* slot);
+void pm_mps_hip_auto_register(PmMpsElem* slot);
 
 /* ---- 2. batch / introspection ----------------------------------------- */
 
@@ -123,8 +129,12 @@ uint32_t pm_hip_n_patterns(void* obj);
 uint32_t pm_hip_max_pattern_len(void* obj);
 /* gid (1..n) -> 0-based add_pattern order; returns UINT32_MAX if out of range */
 uint32_t pm_hip_gid_index(void* obj, uint32_t gid);
-/* Which kernel a compiled object runs: 1 = reverse trie, 2 = AC DFA. */
+/* Which kernel a compiled object runs: 1 = reverse trie, 2 = AC DFA,
+ * 3 = auto (both, picked per launch). */
 int pm_hip_kernel_kind(void* obj);
+/* The kernel of the object's last launch: 1 = reverse trie, 2 = AC DFA
+ * (0 before any). */
+int pm_hip_kernel_last(void* obj);
 /* Seconds of device time of the scan kernels issued through read_block
  * since the last reset (hipEvent based). */
 double pm_hip_device_seconds(void* obj);

@@ -52,12 +52,15 @@ typedef struct {
 } PmMpsInstance;
 
 /* Algorithms of this build (mps.h:20-25 pattern: append before PM_MPS_SIZE).
- * Both are GPU matchers with the exact read_char contract:
- *   PM_MPS_HIP_RT  reverse-suffix-trie walk, one lane per stream position
- *   PM_MPS_HIP_AC  Aho-Corasick dense DFA, one lane per stream segment */
+ * All are GPU matchers with the exact read_char contract:
+ *   PM_MPS_HIP_RT    reverse-suffix-trie walk, one lane per stream position
+ *   PM_MPS_HIP_AC    Aho-Corasick dense DFA, one lane per stream segment
+ *   PM_MPS_HIP_AUTO  both, the kernel picked per block by the RT kernel's
+ *                    measured spill rate (dense deep matches -> AC) */
 enum {
     PM_MPS_HIP_RT = 0,
     PM_MPS_HIP_AC,
+    PM_MPS_HIP_AUTO,
     PM_MPS_SIZE
 };
 

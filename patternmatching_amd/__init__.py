@@ -20,7 +20,8 @@ from .matcher import (  # noqa: F401
     parse_line,
     KIND_RT,
     KIND_AC,
+    KIND_AUTO,
 )
 
-__all__ = ["load", "Dictionary", "HipMatcher", "gen_stream", "parse_line", "KIND_RT", "KIND_AC",
+__all__ = ["load", "Dictionary", "HipMatcher", "gen_stream", "parse_line", "KIND_RT", "KIND_AC", "KIND_AUTO",
            "LIB_PATH", "CLI_PATH"]

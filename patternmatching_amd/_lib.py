@@ -71,6 +71,7 @@ SIGNATURES = {
     # plugin ABI
     "pm_hip_rt_create": (c_vp, []),
     "pm_hip_ac_create": (c_vp, []),
+    "pm_hip_auto_create": (c_vp, []),
     "pm_hip_add_pattern": (None, [c_vp, ctypes.c_char_p, ctypes.c_size_t, c_vp]),
     "pm_hip_compile": (None, [c_vp]),
     "pm_hip_read_char": (c_vp, [c_vp, ctypes.c_char]),
@@ -98,6 +99,7 @@ SIGNATURES = {
     "pm_hip_max_pattern_len": (ctypes.c_uint32, [c_vp]),
     "pm_hip_gid_index": (ctypes.c_uint32, [c_vp, ctypes.c_uint32]),
     "pm_hip_kernel_kind": (ctypes.c_int, [c_vp]),
+    "pm_hip_kernel_last": (ctypes.c_int, [c_vp]),
     "pm_hip_device_seconds": (ctypes.c_double, [c_vp]),
     "pm_hip_table_bytes": (ctypes.c_size_t, [c_vp]),
     "pm_hip_last_error": (ctypes.c_char_p, []),

@@ -48,7 +48,7 @@ static void usage(const char* prog) {
     fprintf(stderr, "  -s FILE               use FILE as one of the stream files (can be used many times).\n");
     fprintf(stderr, "  -o FILE               set FILE to be the output file.\n");
     fprintf(stderr, "  -v                    set verbose to true (print more information)\n");
-    fprintf(stderr, "  -a LIST               algorithms: rt, ac or all (comma separated; default all)\n");
+    fprintf(stderr, "  -a LIST               algorithms: rt, ac, auto or all (comma separated; default all)\n");
     fprintf(stderr, "  -B BYTES              stream chunk per read_block call (default 16777216)\n");
     fprintf(stderr, "  -g DEVICE             HIP device index (default 0)\n");
     fprintf(stderr, "  -m FILE               dump per-position (file<<24|line) u32 codes of the first algorithm\n");
@@ -97,6 +97,7 @@ int pm_parse_args(int argc, char** argv, PmConf* conf) {
                 if (!strcmp(tok, "all")) mask |= (1 << PM_MPS_SIZE) - 1;
                 else if (!strcmp(tok, "rt")) mask |= 1 << PM_MPS_HIP_RT;
                 else if (!strcmp(tok, "ac")) mask |= 1 << PM_MPS_HIP_AC;
+                else if (!strcmp(tok, "auto")) mask |= 1 << PM_MPS_HIP_AUTO;
                 else {
                     fprintf(stderr, "Unknown algorithm %s.\n\n", tok);
                     free(s);

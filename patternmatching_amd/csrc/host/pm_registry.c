@@ -11,4 +11,5 @@ PmMpsElem pm_mps_table[PM_MPS_SIZE];
 void pm_mps_table_setup(void) {
     pm_mps_hip_rt_register(&pm_mps_table[PM_MPS_HIP_RT]);
     pm_mps_hip_ac_register(&pm_mps_table[PM_MPS_HIP_AC]);
+    pm_mps_hip_auto_register(&pm_mps_table[PM_MPS_HIP_AUTO]);
 }

@@ -15,6 +15,7 @@ struct RtDev {
     uint32_t* spill;       // spill_cap 8-B items: per-wave regions of overflow candidates (scratch)
     int64_t spill_cap;     // items
     int64_t spill_stride;  // items per wave region, set per launch
+    unsigned long long* spill_total;  // when set: += items spilled (the auto kernel choice)
     uint32_t t3h_bits;
 };
 

@@ -854,6 +854,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             issue(rs, qn);
             consume(rs);
         }
+        if (t.spill_total && sn && lane == 0) atomicAdd(t.spill_total, (unsigned long long)sn);
         // every placeholder and spill store of this wave complete before
         // its walks patch or read them
         __builtin_amdgcn_s_waitcnt(0);

@@ -46,7 +46,27 @@ thread_local char g_err[512] = "";
         if (e_ != hipSuccess) fatal(#call, e_);   \
     } while (0)
 
-enum Kind { KIND_RT = 1, KIND_AC = 2 };
+enum Kind { KIND_RT = 1, KIND_AC = 2, KIND_AUTO = 3 };
+
+// KIND_AUTO holds both images and picks a kernel per launch: the RT kernel
+// reports how many candidates it spilled (its queue overflowed: dense deep
+// matches, where the AC-DFA kernel is faster -- DESIGN.md §4); when a
+// launch spilled more than AUTO_SPILL_FRAC of its positions, the next
+// AUTO_HOLD launches run the DFA kernel, then one runs RT again to
+// re-measure.  The spill count comes back asynchronously (pinned memory +
+// event): a launch never waits for it.  reset() (a new stream) clears it.
+constexpr double AUTO_SPILL_FRAC = 0.10;
+constexpr int AUTO_HOLD = 64;
+
+struct AutoPick {
+    unsigned long long* d_spill = nullptr;  // device counter of the last RT launch
+    unsigned long long* h_spill = nullptr;  // pinned copy
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+    int64_t n_last = 0;
+    int dfa_left = 0;
+    int last = 0;  // kernel of the last launch (KIND_RT / KIND_AC)
+};
 
 // read_block pipeline blocks (positions): the upload, kernel and download of
 // block k overlap the host finishing block k-1.  Gid output
@@ -68,6 +88,7 @@ struct PipeSlot {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint32_t* spill = nullptr;  // RT deep-walk scratch of this slot's launches
     int64_t spill_cap = 0;
+    AutoPick pick;
     bool busy = false;
     size_t off = 0, m = 0;  // block = positions [off, off + m) of the call
 };
@@ -99,7 +120,16 @@ struct PmHip {
     std::vector<pm_pattern_id_t> id_of_gid;  // [0] = PM_NULL_PATTERN_ID
     PipeSlot slot[2];
     double dev_seconds = 0.0;
+    AutoPick pick;        // scan_device launches (read_block slots have their own)
+    int last_kernel = 0;  // KIND_RT / KIND_AC of the last launch
 };
+
+void free_pick(AutoPick& a) {
+    if (a.d_spill) (void)hipFree(a.d_spill);
+    if (a.h_spill) (void)hipHostFree(a.h_spill);
+    if (a.ev) (void)hipEventDestroy(a.ev);
+    a = AutoPick();
+}
 
 void* dalloc_copy(PmHip* o, const void* src, size_t bytes) {
     void* p = nullptr;
@@ -133,6 +163,7 @@ void free_slot(PipeSlot& q) {
         (void)hipHostFree(q.h_res);
     }
     if (q.spill) (void)hipFree(q.spill);
+    free_pick(q.pick);
     q.d_stage = nullptr;
     q.spill = nullptr;
     q.spill_cap = 0;
@@ -143,7 +174,7 @@ void free_slot(PipeSlot& q) {
 // of a launch, grown to the largest launch seen (scratch, not part of the
 // automaton's total_mem).
 void ensure_spill(PmHip* o, uint32_t*& buf, int64_t& cap, int64_t n) {
-    if (o->kind != KIND_RT) return;
+    if (o->kind != KIND_RT && o->kind != KIND_AUTO) return;
     const int64_t need = pm_rt_spill_items(n, o->num_cu);
     if (need <= cap) return;
     if (buf) PM_CHECK(hipFree(buf));
@@ -202,14 +233,38 @@ void par_range(size_t n, size_t grain, const F& f) {
 }
 
 hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
-                  unsigned long long* count, hipStream_t s, uint32_t* spill, int64_t spill_cap) {
-    if (o->kind == KIND_RT) {
-        RtDev t = o->rt;
-        t.spill = spill;
-        t.spill_cap = spill_cap;
-        return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
+                  unsigned long long* count, hipStream_t s, uint32_t* spill, int64_t spill_cap, AutoPick& ap) {
+    RtDev t = o->rt;
+    t.spill = spill;
+    t.spill_cap = spill_cap;
+    if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
+    if (o->kind == KIND_AC) return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+    // KIND_AUTO
+    if (!ap.ev) {
+        PM_CHECK(hipMalloc(&ap.d_spill, sizeof(unsigned long long)));
+        PM_CHECK(hipHostMalloc(&ap.h_spill, sizeof(unsigned long long), hipHostMallocDefault));
+        PM_CHECK(hipEventCreateWithFlags(&ap.ev, hipEventDisableTiming));
     }
-    return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+    if (ap.pending && hipEventQuery(ap.ev) == hipSuccess) {
+        ap.pending = false;
+        if ((double)*ap.h_spill > AUTO_SPILL_FRAC * (double)ap.n_last) ap.dfa_left = AUTO_HOLD;
+    }
+    if (ap.dfa_left > 0) {
+        --ap.dfa_left;
+        ap.last = KIND_AC;
+        return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+    }
+    ap.last = KIND_RT;
+    t.spill_total = ap.d_spill;
+    hipError_t e = hipMemsetAsync(ap.d_spill, 0, sizeof(unsigned long long), s);
+    if (e == hipSuccess) e = pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
+    if (e == hipSuccess && !ap.pending) {
+        e = hipMemcpyAsync(ap.h_spill, ap.d_spill, sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipEventRecord(ap.ev, s);
+        ap.pending = e == hipSuccess;
+        ap.n_last = n;
+    }
+    return e;
 }
 
 // Scan n new bytes after the carried history.  Results go to out_gid (gids)
@@ -267,7 +322,8 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
         PM_CHECK(hipEventRecord(q.ev0, q.stream));
         PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, 4, nullptr, q.stream,
-                        q.spill, q.spill_cap));
+                        q.spill, q.spill_cap, q.pick));
+        o->last_kernel = q.pick.last ? q.pick.last : o->kind;
         PM_CHECK(hipEventRecord(q.ev1, q.stream));
         PM_CHECK(hipMemcpyAsync(out_gid ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
                                 hipMemcpyDeviceToHost, q.stream));
@@ -311,6 +367,7 @@ const char* pm_hip_last_error(void) { return g_err; }
 
 void* pm_hip_rt_create(void) { return create(KIND_RT); }
 void* pm_hip_ac_create(void) { return create(KIND_AC); }
+void* pm_hip_auto_create(void) { return create(KIND_AUTO); }
 
 void pm_hip_add_pattern(void* obj, char* pat, size_t len, pm_pattern_id_t id) {
     PmHip* o = as(obj);
@@ -333,14 +390,15 @@ void pm_hip_compile(void* obj) {
     const char* env = std::getenv("PM_IMAGE_CACHE");
     const std::string dir = !o->cache_dir.empty() ? o->cache_dir : (env ? env : "");
     bool hit = false;
-    PmImages im = pm_build_images_cached(o->pats, o->gids, o->kind, dir, &hit);
-    if (o->kind == KIND_RT && !im.rt.fits) {
+    const int first = o->kind == KIND_AC ? KIND_AC : KIND_RT;  // AUTO: the RT image, then the DFA's
+    PmImages im = pm_build_images_cached(o->pats, o->gids, first, dir, &hit);
+    if (first == KIND_RT && !im.rt.fits) {
         std::fprintf(stderr, "pm_hip: dictionary exceeds the reverse-trie u16 encoding; using the DFA kernel\n");
         o->kind = KIND_AC;
-        im = pm_build_images_cached(o->pats, o->gids, o->kind, dir, &hit);
+        im = pm_build_images_cached(o->pats, o->gids, KIND_AC, dir, &hit);
     }
     o->cache_hit = hit;
-    if (o->kind == KIND_RT) {
+    if (o->kind == KIND_RT || o->kind == KIND_AUTO) {
         o->rt.t12 = (const uint16_t*)dalloc_copy(o, im.rt.t12.data(), im.rt.t12.size() * 2);
         o->rt.filt = (const uint32_t*)dalloc_copy(o, im.rt.filt.data(), im.rt.filt.size() * 4);
         o->rt.t3h = (const uint4*)dalloc_copy(o, im.rt.t3h.data(), im.rt.t3h.size() * 4);
@@ -349,7 +407,14 @@ void pm_hip_compile(void* obj) {
         o->rt.wide = (const uint4*)dalloc_copy(o, im.rt.wide.data(), im.rt.wide.size() * 4);
         const std::vector<uint8_t> zero(RT_SCRATCH_BYTES, 0);
         o->rt.scratch = (uint32_t*)dalloc_copy(o, zero.data(), zero.size());
-    } else {
+    }
+    if (o->kind == KIND_AUTO) {
+        bool hit2 = false;
+        PmImages d = pm_build_images_cached(o->pats, o->gids, KIND_AC, dir, &hit2);
+        o->cache_hit = hit && hit2;
+        im.dfa = std::move(d.dfa);
+    }
+    if (o->kind == KIND_AC || o->kind == KIND_AUTO) {
         o->dfa.next = (const uint32_t*)dalloc_copy(o, im.dfa.next.data(), im.dfa.next.size() * 4);
         o->dfa.out = (const uint32_t*)dalloc_copy(o, im.dfa.out.data(), im.dfa.out.size() * 4);
         o->dfa.warm = o->max_len ? (int64_t)o->max_len - 1 : 0;
@@ -389,6 +454,8 @@ void pm_hip_reset(void* obj) {
     PmHip* o = as(obj);
     o->hist.clear();
     o->dev_seconds = 0.0;
+    // a new stream: the auto kernel choice is measured again
+    for (PipeSlot& q : o->slot) q.pick.dfa_left = 0;
 }
 
 void pm_hip_free(void* obj) {
@@ -396,6 +463,7 @@ void pm_hip_free(void* obj) {
     (void)hipSetDevice(o->device);
     for (void* p : o->allocs) (void)hipFree(p);
     if (o->spill) (void)hipFree(o->spill);
+    free_pick(o->pick);
     for (PipeSlot& q : o->slot) {
         free_slot(q);
         if (q.ev0) (void)hipEventDestroy(q.ev0);
@@ -419,6 +487,7 @@ static void fill_slot(PmMpsElem* slot, const char* name, void* (*create_fn)(void
 
 void pm_mps_hip_rt_register(PmMpsElem* slot) { fill_slot(slot, "HIP Reverse-Trie", pm_hip_rt_create); }
 void pm_mps_hip_ac_register(PmMpsElem* slot) { fill_slot(slot, "HIP Aho-Corasick DFA", pm_hip_ac_create); }
+void pm_mps_hip_auto_register(PmMpsElem* slot) { fill_slot(slot, "HIP Auto (RT / AC per launch)", pm_hip_auto_create); }
 
 static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, int64_t pos0, int64_t n, void* d_out,
                        int outw, unsigned long long* d_count, void* hip_stream) {
@@ -438,7 +507,8 @@ static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
     if (e == hipSuccess) {
         ensure_spill(o, o->spill, o->spill_cap, n);
         e = launch(o, d_text, stream_start, pos0, n, d_out, outw, d_count, (hipStream_t)hip_stream, o->spill,
-                   o->spill_cap);
+                   o->spill_cap, o->pick);
+        o->last_kernel = o->pick.last ? o->pick.last : o->kind;
     }
     if (e != hipSuccess) {
         std::snprintf(g_err, sizeof(g_err), "launch: %s", hipGetErrorString(e));
@@ -508,7 +578,7 @@ uint32_t pm_hip_parent_gid(void* obj, uint32_t gid) {
 int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out, int out_width,
                               unsigned long long* d_count, void* hip_stream) {
     PmHip* o = as(obj);
-    if (o->kind != KIND_RT) return -1;
+    if (o->kind != KIND_RT && o->kind != KIND_AUTO) return -1;
     ensure_spill(o, o->spill, o->spill_cap, n);
     RtDev t = o->rt;
     t.spill = o->spill;
@@ -542,6 +612,7 @@ uint32_t pm_hip_gid_index(void* obj, uint32_t gid) {
     return o->gids.index_of_gid[gid];
 }
 int pm_hip_kernel_kind(void* obj) { return as(obj)->kind; }
+int pm_hip_kernel_last(void* obj) { return as(obj)->last_kernel; }
 double pm_hip_device_seconds(void* obj) { return as(obj)->dev_seconds; }
 size_t pm_hip_table_bytes(void* obj) { return as(obj)->table_bytes; }
 

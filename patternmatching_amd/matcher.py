@@ -21,6 +21,7 @@ from ._lib import load, PmPattern
 
 KIND_RT = 1
 KIND_AC = 2
+KIND_AUTO = 3
 
 
 def parse_line(line: bytes):
@@ -104,12 +105,15 @@ def gen_stream(n, seed, mode=0, offset=0):
 
 
 class HipMatcher:
-    """One GPU matcher instance ("rt" = reverse-trie kernel, "ac" = AC DFA)."""
+    """One GPU matcher instance ("rt" = reverse-trie kernel, "ac" = AC DFA,
+    "auto" = both, picked per launch)."""
 
     def __init__(self, kind="rt"):
         self.lib = load()
         self.kind_name = kind
-        self.obj = self.lib.pm_hip_rt_create() if kind == "rt" else self.lib.pm_hip_ac_create()
+        create = {"rt": self.lib.pm_hip_rt_create, "ac": self.lib.pm_hip_ac_create,
+                  "auto": self.lib.pm_hip_auto_create}[kind]
+        self.obj = create()
         self._codes = None
         self._dict = None
 
@@ -206,6 +210,11 @@ class HipMatcher:
     @property
     def kernel_kind(self):
         return self.lib.pm_hip_kernel_kind(self.obj)
+
+    @property
+    def kernel_last(self):
+        """Kernel of the last launch: 1 = reverse trie, 2 = AC DFA."""
+        return self.lib.pm_hip_kernel_last(self.obj)
 
     @property
     def max_pattern_len(self):

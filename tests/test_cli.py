@@ -20,7 +20,7 @@ def test_cli_usage_errors():
 
 @pytest.mark.gpu
 def test_cli_et_shipped_stream(tmp_path):
-    """BASELINE config 1 through the drop-in CLI: both GPU matchers, scored
+    """BASELINE config 1 through the drop-in CLI: every GPU matcher, scored
     against the reliable instance (0 FP/FN/partial), dump == golden."""
     csv = tmp_path / "res.csv"
     dump = tmp_path / "m.u32"
@@ -32,7 +32,7 @@ def test_cli_et_shipped_stream(tmp_path):
     assert lines[0].startswith("Algorithm,Time (in secs),Total Memory Used,False Positive Rate,"
                                "False Negative Rate,Partial Success Rate")
     rows = {l.split(",")[0]: l.split(",") for l in lines[1:]}
-    assert set(rows) == {"HIP Reverse-Trie", "HIP Aho-Corasick DFA"}
+    assert set(rows) == {"HIP Reverse-Trie", "HIP Aho-Corasick DFA", "HIP Auto (RT / AC per launch)"}
     for row in rows.values():
         assert row[3:6] == ["0.000000", "0.000000", "0.000000"]
         assert int(row[9]) == 2 * 10240

@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
 SHIP = np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8)
-KINDS = ["rt", "ac"]
+KINDS = ["rt", "ac", "auto"]
+KIND_OF = {"rt": pm.KIND_RT, "ac": pm.KIND_AC, "auto": pm.KIND_AUTO}
 
 _m = {}
 
@@ -24,7 +25,7 @@ def matcher(key, kind):
         m = pm.HipMatcher(kind)
         m.add_dictionary(d)
         m.compile()
-        assert m.kernel_kind == (pm.KIND_RT if kind == "rt" else pm.KIND_AC)
+        assert m.kernel_kind == KIND_OF[kind]
         _m[(key, kind)] = m
     m = _m[(key, kind)]
     m.reset()
@@ -584,3 +585,60 @@ def test_score_and_counts_ragged_lengths(n):
         np.add.at(exp, cur, 1)
         cur = parent[cur]
     assert np.array_equal(hist.cpu().numpy(), exp)
+
+
+def _tiled_ship(n):
+    return np.tile(SHIP, n // len(SHIP) + 1)[:n]
+
+
+def test_auto_switches_to_the_dfa_on_dense_deep_matches():
+    """The auto kind runs RT first; on the reference's shipped stream (dense
+    deep matches: the RT kernel spills > 10 % of positions) the next launches
+    run the AC-DFA kernel, and every launch is exact."""
+    import torch
+    n = 16 << 20
+    text = _tiled_ship(n)
+    s = torch.cuda.current_stream()
+    dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    ref = matcher("et", "ac")
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
+    m = matcher("et", "auto")
+    kernels = []
+    for _ in range(4):
+        got = torch.empty(n, dtype=torch.int32, device="cuda")
+        m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
+        torch.cuda.synchronize()
+        kernels.append(m.kernel_last)
+        assert torch.equal(got, want)
+    assert kernels[0] == pm.KIND_RT and kernels[-1] == pm.KIND_AC, kernels
+
+
+def test_auto_stays_on_rt_for_sparse_matches():
+    import torch
+    n = 16 << 20
+    s = torch.cuda.current_stream()
+    lib = pm.load()
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    assert lib.pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 5, 0, s.cuda_stream) == 0
+    m = matcher("snort", "auto")
+    ref = matcher("snort", "rt")
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
+    for _ in range(4):
+        got = torch.empty(n, dtype=torch.int32, device="cuda")
+        m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
+        torch.cuda.synchronize()
+        assert m.kernel_last == pm.KIND_RT
+        assert torch.equal(got, want)
+
+
+def test_auto_read_block_over_deep_then_sparse_blocks():
+    """read_block through the auto kind: 64 MiB of the shipped stream then
+    random ASCII, in 8 MiB calls (blocks switch kernels), equal to the AC
+    kind's codes everywhere."""
+    text = np.concatenate([_tiled_ship(40 << 20), pm.gen_stream(24 << 20, seed=9, mode=0)])
+    a = matcher("et", "auto")
+    r = matcher("et", "ac")
+    for k in range(0, len(text), 8 << 20):
+        assert np.array_equal(a.read_block_codes(text[k:k + (8 << 20)]), r.read_block_codes(text[k:k + (8 << 20)])), k
