@@ -288,9 +288,9 @@ def main():
                 "dict": args.dict,
                 "stream_bytes_per_gpu": n,
                 "mode": args.mode,
-                "kernel": {"rt": "reverse-suffix-trie walk", "ac": "Aho-Corasick dense DFA",
-                           "auto": "auto: RT or AC-DFA per launch by the RT spill rate (last launch: %s)"
-                                   % {1: "RT", 2: "AC"}.get(m.kernel_last, "?")}[args.kernel],
+                "kernel": ("auto: RT or AC-DFA per launch by the RT spill rate (last launch: %s)"
+                           % {1: "RT", 2: "AC"}.get(m.kernel_last, "?") if args.kernel == "auto" else
+                           {"rt": "reverse-suffix-trie walk", "ac": "Aho-Corasick dense DFA"}[args.kernel]),
                 "parallelism": (f"independent stream shards x{world}" if args.layout == "shards" else
                                 f"one {world * args.bytes} B stream split x{world} (max_len-1 B context per shard)"),
                 "layout": args.layout,

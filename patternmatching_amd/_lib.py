@@ -142,8 +142,8 @@ def load():
                            "(or __graft_entry__.build()); there is no CPU fallback")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        if name.startswith("pm_hip_debug_") and not hasattr(lib, name):
-            continue  # timing hooks: older builds under A/B comparison may lack one
+        if not hasattr(lib, name) and (name.startswith("pm_hip_debug_") or os.environ.get("PM_LIBPM")):
+            continue  # an older build under A/B comparison (PM_LIBPM) may lack a newer entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -111,9 +111,8 @@ class HipMatcher:
     def __init__(self, kind="rt"):
         self.lib = load()
         self.kind_name = kind
-        create = {"rt": self.lib.pm_hip_rt_create, "ac": self.lib.pm_hip_ac_create,
-                  "auto": self.lib.pm_hip_auto_create}[kind]
-        self.obj = create()
+        self.obj = getattr(self.lib, {"rt": "pm_hip_rt_create", "ac": "pm_hip_ac_create",
+                                      "auto": "pm_hip_auto_create"}[kind])()
         self._codes = None
         self._dict = None
 
