@@ -271,17 +271,20 @@ int pm_write_stats(const PmConf* conf, const PmInstanceStats* stats) {
         }
     }
     put(fd, "Algorithm,Time (in secs),Total Memory Used,False Positive Rate,False Negative Rate,"
-            "Partial Success Rate,Device Time (in secs),Device GB/s,Non-null Positions,Bytes");
+            "Partial Success Rate,Device Time (in secs),Device GB/s,Non-null Positions,Bytes,"
+            "Device Roofline Fraction,GPU");
     for (int a = 0; a < PM_MPS_SIZE; ++a) {
         const PmInstanceStats* s = &stats[a];
         if (!(conf->algo_mask & (1 << a))) continue;
         uint64_t sum = s->sr.success + s->sr.false_pos + s->sr.false_neg + s->sr.partial_suc;
         long double den = sum ? (long double)sum : 1.0L;
-        snprintf(buf, sizeof(buf), "\n%s,%.6f,%zu,%.6Lf,%.6Lf,%.6Lf,%.6f,%.3f,%llu,%llu", pm_mps_table[a].name,
+        /* roofline: 5 algorithmic bytes per position (1 read + the u32 id
+         * read_block writes) over the device time, against 8 TB/s HBM */
+        const double dev_gbs = s->device_seconds > 0 ? (double)s->bytes / s->device_seconds / 1e9 : 0.0;
+        snprintf(buf, sizeof(buf), "\n%s,%.6f,%zu,%.6Lf,%.6Lf,%.6Lf,%.6f,%.3f,%llu,%llu,%.6g,%d", pm_mps_table[a].name,
                  s->wall_seconds, s->total_mem, (long double)s->sr.false_pos / den,
-                 (long double)s->sr.false_neg / den, (long double)s->sr.partial_suc / den, s->device_seconds,
-                 s->device_seconds > 0 ? (double)s->bytes / s->device_seconds / 1e9 : 0.0,
-                 (unsigned long long)s->nonnull, (unsigned long long)s->bytes);
+                 (long double)s->sr.false_neg / den, (long double)s->sr.partial_suc / den, s->device_seconds, dev_gbs,
+                 (unsigned long long)s->nonnull, (unsigned long long)s->bytes, dev_gbs * 5.0 / 8000.0, conf->device);
         put(fd, buf);
     }
     put(fd, "\n");

@@ -36,6 +36,7 @@ def test_cli_et_shipped_stream(tmp_path):
     for row in rows.values():
         assert row[3:6] == ["0.000000", "0.000000", "0.000000"]
         assert int(row[9]) == 2 * 10240
+        assert len(row) == 12 and 0.0 < float(row[10]) < 1.0 and row[11] == "0"  # roofline frac, GPU id
     gold = np.fromfile(os.path.join(GOLDEN, "ship_et.u32"), dtype="<u4")
     got = np.fromfile(dump, dtype="<u4")
     assert np.array_equal(got, np.concatenate([gold, gold]))  # reset per stream file
