@@ -343,14 +343,22 @@ PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap&
 
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
     DfaImage im;
-    BfsTrie t = build_trie(pats, g, /*reversed=*/false);
+    BfsTrie t = build_trie(pats, g, /*reversed=*/false, PM_DFA_DFS_DEPTH);
     const uint32_t S = t.n;
     im.states = S;
     im.next.assign((size_t)S * 256, 0);
     im.out.assign(S, 0);
     std::vector<uint32_t> fail(S, 0);
-    // BFS order guarantees fail[v] (shallower) has its row before v's.
+    // rows in breadth-first order (by depth), so fail[v] (shallower) has its
+    // row before v's whatever the numbering below PM_DFA_DFS_DEPTH
+    std::vector<uint32_t> by_depth(S), dstart;
     for (uint32_t v = 0; v < S; ++v) {
+        if (t.depth[v] + 2 > dstart.size()) dstart.resize(t.depth[v] + 2, 0);
+        dstart[t.depth[v] + 1]++;
+    }
+    for (size_t d = 1; d < dstart.size(); ++d) dstart[d] += dstart[d - 1];
+    for (uint32_t v = 0; v < S; ++v) by_depth[dstart[t.depth[v]]++] = v;
+    for (uint32_t v : by_depth) {
         uint32_t* row = &im.next[(size_t)v * 256];
         if (v) std::memcpy(row, &im.next[(size_t)fail[v] * 256], 256 * sizeof(uint32_t));
         for (uint32_t k = 0; k < t.ccount[v]; ++k) {
@@ -525,7 +533,7 @@ uint64_t pm_image_key(const std::vector<std::string>& pats, int kind) {
     // few keys): a change to either gives new keys, not a stale hit
     uint32_t lay[] = {RT_T1_BASE, RT_CONT16, RT_CONT32, (uint32_t)RT_REC_WORDS, RT_FILTER_WORDS, RT_F3_WORDS,
                       RT_F4_WORDS, RT_T3H_INLINE, RT_T3H_VALID, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                      RT_REC_INLINE, (uint32_t)RT_WIDE_WORDS};
+                      RT_REC_INLINE, (uint32_t)RT_WIDE_WORDS, (uint32_t)PM_DFA_DFS_DEPTH};
     const uint32_t probe[2] = {0x00A1B2C3u, 0x00FFFFFFu};
     for (int q = 0; q < 2; ++q) {
         const uint32_t k = probe[q];

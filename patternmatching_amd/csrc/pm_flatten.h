@@ -138,6 +138,11 @@ constexpr int RT_REC_WORDS = 4;
 constexpr uint32_t RT_REC_LEAF = 0, RT_REC_KIDS = 1, RT_REC_WIDE = 3;  // record kinds (x >> 30)
 constexpr uint32_t RT_REC_INLINE = 8;  // children held inline in a record
 constexpr int RT_WIDE_WORDS = 16;
+// DFA state numbering: breadth-first to this depth, then children blocks in
+// depth-first order (build_trie), so a pattern's deep states are neighbours
+#ifndef PM_DFA_DFS_DEPTH
+#define PM_DFA_DFS_DEPTH 0xFFFFFFFFu
+#endif
 inline uint32_t pm_rt_wide_word(uint32_t w) { return 4 * (w >> 1) + (w & 1); }  // bitmap word w in an entry
 constexpr uint32_t RT_FILTER_WORDS = 4096;  // stage 1: 16 KiB of LDS
 constexpr uint32_t RT_F3_WORDS = 256;       // stage 2, 3-byte patterns: 1 KiB

@@ -8,7 +8,7 @@ OUT=$(pwd)/gpurun_out; TAG=$1; ARGS=$2; shift 2; mkdir -p "$OUT"
 for pass in 1 2 3; do
   for lib in "$@"; do
     for mode in ${AB_MODES:-dense dense16 count}; do
-      PM_LIBPM=$(pwd)/$lib timeout -k 10 300 python bench.py --no-cpu --steps 10 --mode $mode $ARGS > "$OUT/abb_tmp.json" 2>/dev/null || { echo fail $lib; exit 1; }
+      PM_LIBPM=$(pwd)/$lib timeout -k 10 300 python bench.py --no-cpu --steps 10 --mode $mode $ARGS > "$OUT/abb_tmp.json" 2>"$OUT/abb_err.txt" || { echo fail $lib; tail -5 "$OUT/abb_err.txt"; exit 1; }
       python3 -c "
 import json; d=json.load(open('$OUT/abb_tmp.json'))
 print('$pass', '$lib', '$mode', d['kernel_ms'], d['value'])" | tee -a "$OUT/abb_$TAG.txt"
