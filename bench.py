@@ -244,10 +244,12 @@ def main():
                                  "score_ms": round(e0.elapsed_time(e1), 4)}
             del ref
             hist = torch.zeros(lib.pm_hip_n_patterns(m.obj) + 1, dtype=torch.int64, device="cuda")
-            e0.record(stream)
-            m.pattern_counts_device(out.data_ptr(), n, hist.data_ptr(), stream.cuda_stream)
-            e1.record(stream)
-            torch.cuda.synchronize()
+            for _ in range(2):  # the second launch is timed (the first pays first-touch costs)
+                hist.zero_()
+                e0.record(stream)
+                m.pattern_counts_device(out.data_ptr(), n, hist.data_ptr(), stream.cuda_stream)
+                e1.record(stream)
+                torch.cuda.synchronize()
             extra["pattern_counts"] = {"patterns_seen": int((hist > 0).sum().item()),
                                        "occurrences": int(hist.sum().item()),
                                        "ms": round(e0.elapsed_time(e1), 4)}

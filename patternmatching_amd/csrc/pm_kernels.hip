@@ -1030,6 +1030,12 @@ constexpr int HIST_V = 4;  // 16-B answer loads per thread per step (snort 1 GiB
 // Each thread takes V 16-B loads of answers (4V positions) and walks their 4V
 // suffix chains together, so the dependent parent[] gathers of one step are
 // all in flight at once (one chain after another left them latency-bound).
+// Measured and not kept (round 2): a "has parent" bit per gid so that only
+// the ~5% of chains that go on gather parent[] — kept in bit 31 of the
+// counter and read back by the add, 3.40 ms against 1.28 (an LDS add that
+// returns its value waits; one that does not is fire-and-forget), or in an
+// LDS bitmap beside the counters, 1.30-1.32 against 1.28 (the gathers of
+// the ~3,000 gids a stream hits are L1 hits).
 template <int V>
 __global__ __launch_bounds__(HIST_THREADS) void hist_kernel(const uint32_t* __restrict__ real, int64_t n,
                                                             const uint32_t* __restrict__ parent, uint32_t lo,
