@@ -275,7 +275,10 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
 // then the caller's own buffer), staged in pinned memory -- scanned, and the
 // gids downloaded straight into out_gid, or into pinned memory from which
 // the host maps them to pattern ids (threads) while block k+1 is in flight.
-// Measured rates: DESIGN.md §5.
+// For pattern ids, dictionaries of < 65,536 patterns (every reference
+// dictionary) come back as u16 gids (half the PCIe bytes) for the host
+// threads to map: +12% (RT) / +28% (AC).  Gids for the caller stay u32 and
+// direct: widening u16 on the host measured 2-5% slower.  Rates: DESIGN.md §5.
 void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pattern_id_t* out_ids) {
     if (!o->compiled) {
         std::fprintf(stderr, "pm_hip: read before compile\n");
@@ -284,15 +287,22 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
     PM_CHECK(hipSetDevice(o->device));
     const size_t keep = o->max_len ? o->max_len - 1 : 0;
     const size_t pipe = out_gid ? PIPE_GID_POSITIONS : PIPE_ID_POSITIONS;
+    const bool narrow = !out_gid && o->gids.index_of_gid.size() <= 65536;  // u16 gids over PCIe
     auto finish = [&](PipeSlot& q) {
         PM_CHECK(hipStreamSynchronize(q.stream));
         float ms = 0.f;
         PM_CHECK(hipEventElapsedTime(&ms, q.ev0, q.ev1));
         o->dev_seconds += ms * 1e-3;
-        if (!out_gid) {
+        const pm_pattern_id_t* map = o->id_of_gid.data();
+        if (narrow) {
+            const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
+            pm_pattern_id_t* dst = out_ids + q.off;
+            par_range(q.m, (size_t)1 << 18, [&](size_t lo, size_t hi) {
+                for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
+            });
+        } else if (!out_gid) {
             const uint32_t* g = q.h_res;
             pm_pattern_id_t* dst = out_ids + q.off;
-            const pm_pattern_id_t* map = o->id_of_gid.data();
             par_range(q.m, (size_t)1 << 18, [&](size_t lo, size_t hi) {
                 for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
             });
@@ -321,12 +331,15 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         PM_CHECK(hipMemcpyAsync(q.d_stage + ctx, buf + done, m, hipMemcpyHostToDevice, q.stream));
         PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
         PM_CHECK(hipEventRecord(q.ev0, q.stream));
-        PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, 4, nullptr, q.stream,
-                        q.spill, q.spill_cap, q.pick));
+        PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, narrow ? 2 : 4, nullptr,
+                        q.stream, q.spill, q.spill_cap, q.pick));
         o->last_kernel = q.pick.last ? q.pick.last : o->kind;
         PM_CHECK(hipEventRecord(q.ev1, q.stream));
-        PM_CHECK(hipMemcpyAsync(out_gid ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
-                                hipMemcpyDeviceToHost, q.stream));
+        if (narrow)
+            PM_CHECK(hipMemcpyAsync(q.h_res, q.d_res, m * sizeof(uint16_t), hipMemcpyDeviceToHost, q.stream));
+        else
+            PM_CHECK(hipMemcpyAsync(out_gid ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
+                                    hipMemcpyDeviceToHost, q.stream));
         q.busy = true;
         q.off = done;
         q.m = m;
