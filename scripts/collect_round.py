@@ -21,7 +21,8 @@ names = {"dense": "C3 snort 1 GiB dense_u32 (bench default, 16-core reference ba
          "score": "snort 1 GiB dense_u32 + on-device accuracy scoring vs the AC instance (--score)",
          "ship": "snort, the shipped stream tiled to 1 GiB (deep matches), dense_u32",
          "ship_count": "snort, the shipped stream tiled to 1 GiB, count_only",
-         "ship_ac": "snort, the shipped stream tiled to 1 GiB, AC dense DFA, dense_u32"}
+         "ship_ac": "snort, the shipped stream tiled to 1 GiB, AC dense DFA, dense_u32",
+         "ship_auto": "snort, the shipped stream tiled to 1 GiB, auto kind (RT, then AC after a spilling launch), dense_u32"}
 lines = {}
 for k, label in names.items():
     p = os.path.join(src, f"bench_{k}.json")
