@@ -156,6 +156,8 @@ int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int
 /* Launch shape of the AC-DFA kernel for timing sweeps: segments in flight
  * (lanes) per CU; 0 restores the default. */
 void pm_hip_debug_dfa_shape(int lanes_per_cu);
+/* Timing sweeps only: the AC-DFA kernel's shortest segment (0 = default). */
+void pm_hip_debug_dfa_min_seg(int min_seg);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

@@ -108,6 +108,7 @@ SIGNATURES = {
     "pm_hip_debug_scan_variant": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int64, c_vp, ctypes.c_int,
                                                  c_vp, c_vp]),
     "pm_hip_debug_dfa_shape": (None, [ctypes.c_int]),
+    "pm_hip_debug_dfa_min_seg": (None, [ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
     "pm_flat_build_cached": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int,

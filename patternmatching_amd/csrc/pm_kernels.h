@@ -44,6 +44,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 // launch shape of the DFA kernel (timing sweeps): lanes per CU; <= 0
 // restores the default
 void pm_dfa_set_shape(int lanes_per_cu);
+void pm_dfa_set_min_seg(int min_seg);
 // counts[0..4] += success, partial, false_neg, false_pos, all_matches of algo
 // against real (n u32 gids each, 16-B aligned); parent/depth: PmParents.
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,

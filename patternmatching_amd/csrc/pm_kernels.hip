@@ -28,6 +28,8 @@
 //   every segment is independent and exact.
 #include <type_traits>
 
+#include <algorithm>
+
 #include "pm_kernels.h"
 #include "pm_streamgen.h"
 
@@ -1166,17 +1168,26 @@ hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream
 // more distinct table lines than the caches hold.
 constexpr int DFA_LANES_PER_CU = 512;
 static int g_dfa_lanes_per_cu = DFA_LANES_PER_CU;
+// Shortest segment.  A launch of fewer segments than lanes is latency-bound
+// (each lane's chain of max_len-1 warm-up + segment dependent steps is the
+// launch time), so short launches want short segments, at the price of
+// more warm-up steps: n / 65536 clamped to [64, 512] bytes.  Measured
+// (scripts/dfa_seg_sweep.py, profiles/r02/dfa_segment_sweep.txt), against
+// the round-1 fixed 2 KiB: 100 KiB 0.34 -> 0.07 ms, 1 MiB 0.62 -> 0.07,
+// 16 MiB 0.76-0.86 -> 0.28-0.37, 64 MiB 1.06-1.43 -> 0.59-0.73; from 256
+// MiB up the lane cap decides and nothing changes.
+static int64_t g_dfa_min_seg = 0;  // pm_dfa_set_min_seg override (timing sweeps)
 
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (!out) outw = 0;
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
-    // one segment per lane, each at least 2 KiB so the max_len-1 warm-up
-    // stays a small fraction
+    // one segment per lane, none shorter than short_seg (above)
     const int64_t lanes = (int64_t)num_cu * g_dfa_lanes_per_cu;
     int64_t seg = (n + lanes - 1) / lanes;
-    if (seg < 2048) seg = 2048;
+    const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
+    if (seg < short_seg) seg = short_seg;
     seg = (seg + 15) & ~(int64_t)15;
     const int64_t nseg = (n + seg - 1) / seg;
     int64_t blocks = (nseg + DFA_THREADS - 1) / DFA_THREADS;
@@ -1192,6 +1203,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 }
 
 void pm_dfa_set_shape(int lanes_per_cu) { g_dfa_lanes_per_cu = lanes_per_cu > 0 ? lanes_per_cu : DFA_LANES_PER_CU; }
+void pm_dfa_set_min_seg(int min_seg) { g_dfa_min_seg = min_seg >= 16 ? min_seg : 0; }
 
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,
                           const uint32_t* depth, unsigned long long* counts, int num_cu, hipStream_t s) {

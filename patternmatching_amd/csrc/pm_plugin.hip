@@ -602,6 +602,7 @@ int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int
 }
 
 void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }
+void pm_hip_debug_dfa_min_seg(int min_seg) { pm_dfa_set_min_seg(min_seg); }
 
 int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
                              void* hip_stream) {
