@@ -75,6 +75,13 @@ struct AutoPick {
 // of that mapping with the transfers.
 constexpr size_t PIPE_GID_POSITIONS = (size_t)16 << 20;
 constexpr size_t PIPE_ID_POSITIONS = (size_t)8 << 20;
+// Blocks up to this size go through the pinned staging buffers both ways
+// (one host memcpy each side, one DMA each way) instead of the runtime's
+// own staging of pageable memory, whose fixed cost per copy dominates a
+// small call such as the reference's 100 KiB chunks (measure.c:284):
+// +10-18% there; at 1 MiB the single-threaded 4 MiB result copy made the
+// gid path 37% slower (profiles/r02/host_path_small_staging_ab.txt).
+constexpr size_t PIPE_SMALL_POSITIONS = (size_t)256 << 10;
 
 // One pipeline slot: pinned host and device staging for one block and its
 // own stream, so two blocks are in flight.
@@ -90,6 +97,7 @@ struct PipeSlot {
     int64_t spill_cap = 0;
     AutoPick pick;
     bool busy = false;
+    bool staged = false;    // small block: results land in h_res, copied out by finish
     size_t off = 0, m = 0;  // block = positions [off, off + m) of the call
 };
 
@@ -306,6 +314,8 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             par_range(q.m, (size_t)1 << 18, [&](size_t lo, size_t hi) {
                 for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
             });
+        } else if (q.staged) {
+            std::memcpy(out_gid + q.off, q.h_res, q.m * sizeof(uint32_t));
         }
         q.busy = false;
     };
@@ -326,10 +336,17 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             std::memcpy(st, o->hist.data() + o->hist.size() - from_hist, from_hist);
             std::memcpy(st + from_hist, buf, done);
         }
-        std::memset(q.h_stage + ctx, 0, 16);
-        if (ctx) PM_CHECK(hipMemcpyAsync(q.d_stage, q.h_stage, ctx, hipMemcpyHostToDevice, q.stream));
-        PM_CHECK(hipMemcpyAsync(q.d_stage + ctx, buf + done, m, hipMemcpyHostToDevice, q.stream));
-        PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
+        q.staged = m <= PIPE_SMALL_POSITIONS;
+        if (q.staged) {  // [context | bytes | 16 zero bytes] in one DMA from pinned memory
+            std::memcpy(q.h_stage + ctx, buf + done, m);
+            std::memset(q.h_stage + ctx + m, 0, 16);
+            PM_CHECK(hipMemcpyAsync(q.d_stage, q.h_stage, ctx + m + 16, hipMemcpyHostToDevice, q.stream));
+        } else {
+            std::memset(q.h_stage + ctx, 0, 16);
+            if (ctx) PM_CHECK(hipMemcpyAsync(q.d_stage, q.h_stage, ctx, hipMemcpyHostToDevice, q.stream));
+            PM_CHECK(hipMemcpyAsync(q.d_stage + ctx, buf + done, m, hipMemcpyHostToDevice, q.stream));
+            PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
+        }
         PM_CHECK(hipEventRecord(q.ev0, q.stream));
         PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, narrow ? 2 : 4, nullptr,
                         q.stream, q.spill, q.spill_cap, q.pick));
@@ -338,7 +355,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         if (narrow)
             PM_CHECK(hipMemcpyAsync(q.h_res, q.d_res, m * sizeof(uint16_t), hipMemcpyDeviceToHost, q.stream));
         else
-            PM_CHECK(hipMemcpyAsync(out_gid ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
+            PM_CHECK(hipMemcpyAsync(out_gid && !q.staged ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
                                     hipMemcpyDeviceToHost, q.stream));
         q.busy = true;
         q.off = done;
