@@ -519,6 +519,40 @@ def test_full_size_merged_4gib_kernels_agree():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("stream", ["bytes", "ship"])
+def test_full_size_binary_and_deep_streams_kernels_agree(stream):
+    """1 GiB of uniform bytes (every byte value, snort's binary patterns) and
+    the shipped adversarial stream tiled to 1 GiB (26% of positions spill to
+    the deep-walk tail): RT, AC and the auto kind agree at every position."""
+    torch = _torch()
+    rt, ac, au = matcher("snort", "rt"), matcher("snort", "ac"), matcher("snort", "auto")
+    n = 1 << 30
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    if stream == "bytes":
+        pm.load().pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 7, 1, s)
+    else:
+        ship = torch.from_numpy(SHIP).cuda()
+        dt.copy_(ship.repeat((n + 64) // len(SHIP) + 1)[: n + 64])
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = torch.empty(n, dtype=torch.int32, device="cuda")
+    ca = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cb = torch.zeros(1, dtype=torch.int64, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), ca.data_ptr(), s)
+    ac.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), cb.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert int(ca.item()) == int(cb.item()) == int((a != 0).sum().item())
+    for _ in range(2):  # auto: an RT launch, then (deep stream) the DFA
+        b.zero_()
+        au.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), None, s)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+    del a, b, dt
+    torch.cuda.empty_cache()
+
+
 def test_adversarial_stream_large_rt_equals_ac():
     """A 32 MiB tiling of the shipped adversarial stream queues far more
     positions than the worklist holds, so the scan kernel's in-kernel
