@@ -481,6 +481,14 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // the plain one-walk-per-lane tail, a cross-check of rt_tail; V = 6:
     // no tail at all, V = 7: the tail's probe phase only; both timing only)
     constexpr bool kFilter = V == 0 || V >= 3;
+    // Stage 2 at push time: only its passers are queued, so rounds are ~3.3x
+    // rarer and all their candidates probe; the lane's loop over its own
+    // candidates costs more than it saves where the kernel is compute-bound.
+    // Side by side (scripts/bench_variants.py, V = 8 for every width):
+    // dense u32 snort 1.141 -> 1.135 ms, merged 1.167 -> 1.149, shipped
+    // stream 12.28 -> 11.52; count 0.785 -> 0.807 and u16 0.830 -> 0.838
+    // on snort.  So the product does it for u32 ids only.
+    constexpr bool kPushS2 = V == 8 || (V == 0 && OUTW == 4);
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -559,7 +567,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         // stage 2 on first probes: only a 3-byte pattern or a depth-4 suffix
         // can change the placeholder, anything else needs no probe
         bool skip = false;
-        if (take) {  // wave-uniform
+        if (!kPushS2 && take) {  // wave-uniform
             const bool first = act && !deep && !(r.fp & RT_SLOT2);
             if (first) skip = rt_stage2_hit(rt_stage2_load(s_f2, r.fk)) == 0u;
         }
@@ -774,6 +782,21 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             }
         }
         asm volatile("" ::: "memory");  // the store stays ahead of any later probe
+        if (kPushS2) {
+            // stage 2 now, over the lane's own candidates: only its passers
+            // are queued (a rejected one keeps its depth-2 placeholder)
+            uint32_t mm = cm, keep = 0;
+            while (mm) {
+                const uint32_t j = __builtin_ctz(mm);
+                mm &= mm - 1;
+                const uint32_t sg = j >> 2, b = j & 3;
+                const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
+                const u32x2 w = (sg & 2) ? w23 : w01;
+                const uint32_t q32 = (uint32_t)((((uint64_t)w.y << 32) | w.x) >> (8 * (1 + b)));
+                keep |= (rt_stage2_hit(rt_stage2_load(s_f2, q32)) != 0u) << j;
+            }
+            cm = keep;
+        }
         if (kFilter) {
             // lane count c = popc(cm); exclusive wave prefix by a DPP scan;
             // items written by a loop over the lane's own set bits
@@ -1146,6 +1169,7 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 5: RT_LAUNCH(5); break;
         case 6: RT_LAUNCH(6); break;
         case 7: RT_LAUNCH(7); break;
+        case 8: RT_LAUNCH(8); break;
         default: RT_LAUNCH(0);
     }
 #undef RT_LAUNCH

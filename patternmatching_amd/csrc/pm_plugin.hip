@@ -484,8 +484,16 @@ void pm_hip_reset(void* obj) {
     PmHip* o = as(obj);
     o->hist.clear();
     o->dev_seconds = 0.0;
-    // a new stream: the auto kernel choice is measured again
-    for (PipeSlot& q : o->slot) q.pick.dfa_left = 0;
+    // a new stream: the auto kernel choice is measured again, for read_block
+    // slots and scan_device launches alike (a spill count still in flight
+    // belongs to the old stream: wait for it and drop it)
+    auto forget = [](AutoPick& a) {
+        if (a.pending) (void)hipEventSynchronize(a.ev);
+        a.pending = false;
+        a.dfa_left = 0;
+    };
+    forget(o->pick);
+    for (PipeSlot& q : o->slot) forget(q.pick);
 }
 
 void pm_hip_free(void* obj) {

@@ -19,6 +19,7 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--stream", type=int, default=0, help="0 ascii, 1 bytes, 2 the shipped stream tiled")
 ap.add_argument("--variants", default="0,1,2")
 ap.add_argument("--modes", default="dense,dense16,count")
+ap.add_argument("--exact", default="", help="variants whose dense u32 ids must equal v0's (checked after timing)")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 WIDTH = {"dense": 4, "dense16": 2, "count": 0}
@@ -57,4 +58,14 @@ for (v, mode), t in times.items():
     ms = statistics.median(t)
     res[f"v{v}-{mode}"] = {"ms": round(ms, 4), "min": round(min(t), 4), "GBps_stream": round(n / ms / 1e6, 1),
                            "alg_GBps": round(n * (1 + WIDTH[mode]) / ms / 1e6, 1)}
+if args.exact:
+    def ids(v):
+        o = torch.zeros(n, dtype=torch.int32, device="cuda")
+        assert lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, o.data_ptr(), 4, cnt.data_ptr(),
+                                             s.cuda_stream) == 0
+        torch.cuda.synchronize()
+        return o
+    ref = ids(0)
+    for v in (int(x) for x in args.exact.split(",")):
+        res[f"v{v}-ids-equal-v0"] = bool(torch.equal(ids(v), ref))
 print(json.dumps(res, indent=1))
