@@ -482,13 +482,19 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // no tail at all, V = 7: the tail's probe phase only; both timing only)
     constexpr bool kFilter = V == 0 || V >= 3;
     // Stage 2 at push time: only its passers are queued, so rounds are ~3.3x
-    // rarer and all their candidates probe; the lane's loop over its own
-    // candidates costs more than it saves where the kernel is compute-bound.
-    // Side by side (scripts/bench_variants.py, V = 8 for every width):
-    // dense u32 snort 1.141 -> 1.135 ms, merged 1.167 -> 1.149, shipped
-    // stream 12.28 -> 11.52; count 0.785 -> 0.807 and u16 0.830 -> 0.838
-    // on snort.  So the product does it for u32 ids only.
-    constexpr bool kPushS2 = V == 8 || (V == 0 && OUTW == 4);
+    // rarer and all their candidates probe.  Rounds in the chunk loop, or
+    // every candidate to the spill region for the tail.  Side by side
+    // (scripts/bench_variants.py; V = 8: push-time stage 2 with rounds, V =
+    // 9: push-time stage 2, no rounds; snort / merged / shipped stream, ms):
+    //   u32   issue-time 1.141 / 1.167 / 12.28   V8 1.135 / 1.149 / 11.52
+    //         V9 1.178 / - / 11.26
+    //   u16   issue-time 0.830 / 0.971 / 11.83   V8 0.838 / 0.970 / 10.57
+    //         V9 0.809 / 1.012 / 10.71
+    //   count issue-time 0.784 / 0.910 / 8.68    V8 0.807 / 0.944 / 8.05
+    //         V9 0.768 / 0.882 / 8.00
+    // So the product: u32 = V8, count = V9, u16 = issue-time stage 2.
+    constexpr bool kPushS2 = V == 8 || V == 9 || (V == 0 && OUTW != 2);
+    constexpr bool kRounds = !(V == 9 || (V == 0 && OUTW == 0));
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -760,7 +766,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             res[j] &= 0x7FFFu;
             scnt += (uint32_t)__popcll(__ballot(res[j] != 0u));
         }
-        if (kFilter) {
+        if (kFilter && kRounds) {
             if (rr.n) consume(rr);                // the round issued last chunk
             issue(rr, qn >= RT_ROUND ? qn : 0u);  // items of earlier chunks (stores issued)
         }
@@ -806,7 +812,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
             uint32_t mm = cm;
             const uint32_t pbase = (uint32_t)(pc - pos0) + 4 * lane;
-            if (total <= RT_QCAP - qn - rr.keep) {
+            if (kRounds && total <= RT_QCAP - qn - rr.keep) {
                 // the whole chunk fits the ring (the in-flight round's
                 // possible survivors keep their room); the window's bytes
                 // i-3..i by one 64-bit shift
@@ -828,7 +834,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 // (in rank order) fill the ring, the rest go to the spill
                 // region, walked after the chunk loop, with whether their
                 // placeholder (t12 of the key) is nonzero
-                const uint32_t room = RT_QCAP - qn - rr.keep;
+                const uint32_t room = kRounds ? RT_QCAP - qn - rr.keep : 0u;
                 uint32_t rank = base;
                 while (mm) {
                     const uint32_t j = __builtin_ctz(mm);
@@ -859,10 +865,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // store, prefetch; round, store, prefetch) so the compiler's vmcnt is the
     // steady-state one.
     Round r0;
-    if (kFilter) issue(r0, 0);
+    if (kFilter && kRounds) issue(r0, 0);
     stand_in_store();
     fetch(xa, pa, ch);
-    if (kFilter) issue(rr, 0);
+    if (kFilter && kRounds) issue(rr, 0);
     stand_in_store();
     fetch(xb, pb, ch + cstep);
     for (;;) {  // wave-uniform
@@ -1170,6 +1176,7 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 6: RT_LAUNCH(6); break;
         case 7: RT_LAUNCH(7); break;
         case 8: RT_LAUNCH(8); break;
+        case 9: RT_LAUNCH(9); break;
         default: RT_LAUNCH(0);
     }
 #undef RT_LAUNCH
