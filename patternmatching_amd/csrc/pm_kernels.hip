@@ -492,9 +492,11 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     //         V9 0.809 / 1.012 / 10.71
     //   count issue-time 0.784 / 0.910 / 8.68    V8 0.807 / 0.944 / 8.05
     //         V9 0.768 / 0.882 / 8.00
-    // So the product: u32 = V8, count = V9, u16 = issue-time stage 2.
-    constexpr bool kPushS2 = V == 8 || V == 9 || (V == 0 && OUTW != 2);
-    constexpr bool kRounds = !(V == 9 || (V == 0 && OUTW == 0));
+    //         V10 (no rounds, stage 2 in the tail's batched probe phase)
+    //         0.733 / 0.832 / 8.63 (V9 on the same box 0.763 / 0.879 / 7.95)
+    // So the product: u32 = V8, count = V10, u16 = issue-time stage 2.
+    constexpr bool kPushS2 = V == 8 || V == 9 || (V == 0 && OUTW == 4);
+    constexpr bool kRounds = !(V == 9 || V == 10 || (V == 0 && OUTW == 0));
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -1177,6 +1179,7 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 7: RT_LAUNCH(7); break;
         case 8: RT_LAUNCH(8); break;
         case 9: RT_LAUNCH(9); break;
+        case 10: RT_LAUNCH(10); break;
         default: RT_LAUNCH(0);
     }
 #undef RT_LAUNCH
