@@ -35,6 +35,13 @@
 
 namespace {
 
+// The chunk's answer stores (A/B builds: -DRT_PLAIN_STORES keeps the lines
+// in L2 for the patches that follow a round later)
+#ifdef RT_PLAIN_STORES
+#define RT_OUT_STORE(v, p) (*(p) = (v))
+#else
+#define RT_OUT_STORE(v, p) __builtin_nontemporal_store((v), (p))
+#endif
 constexpr int RT_THREADS = 1024;
 constexpr int RT_WAVES = RT_THREADS / 64;
 constexpr int RT_T2_U16 = 65536;
@@ -778,7 +785,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 u32x4 v = {res[4 * s], res[4 * s + 1], res[4 * s + 2], res[4 * s + 3]};
-                __builtin_nontemporal_store(v, o + 64 * s + lane);
+                RT_OUT_STORE(v, o + 64 * s + lane);
             }
         }
         if (OUTW == 2) {  // 512 contiguous bytes per store instruction
@@ -786,7 +793,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 u32x2 v = {res[4 * s] | (res[4 * s + 1] << 16), res[4 * s + 2] | (res[4 * s + 3] << 16)};
-                __builtin_nontemporal_store(v, o + 64 * s + lane);
+                RT_OUT_STORE(v, o + 64 * s + lane);
             }
         }
         asm volatile("" ::: "memory");  // the store stays ahead of any later probe
