@@ -274,7 +274,7 @@ struct TailSlot {
 };
 
 template <int OUTW, bool kProbeOnly = false, int SLOTS = RT_TAIL_SLOTS>
-__device__ __forceinline__ void rt_tail(const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0,
+__device__ __forceinline__ uint32_t rt_tail(const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0,
                                         void* __restrict__ out, const RtDev& t, const uint32_t* s_f2,
                                         uint32_t* sp, uint32_t sn, int lane, uint32_t& cnt) {
     const uint8_t* const tb = text + pos0;  // offsets are from pos0; pos0 % 16 == 0
@@ -336,7 +336,7 @@ __device__ __forceinline__ void rt_tail(const uint8_t* __restrict__ text, int64_
             nwalk += (uint32_t)__popcll(m);
         });
     }
-    if (!nwalk || kProbeOnly) return;
+    if (!nwalk || kProbeOnly) return nwalk;
     // the walk entries are stored (vmcnt 0) and this CU's L1 dropped
     // (phase 1 read the same lines before overwriting them) before they are
     // read
@@ -454,6 +454,7 @@ __device__ __forceinline__ void rt_tail(const uint8_t* __restrict__ text, int64_
             z.pb = pb;
         });
     }
+    return nwalk;
 }
 
 template <int V, int OUTW>
@@ -894,7 +895,10 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             issue(rs, qn);
             consume(rs);
         }
-        if (t.spill_total && sn && lane == 0) atomicAdd(t.spill_total, (unsigned long long)sn);
+        // the auto kind's measure of deep matches: items the ring could not
+        // hold; count-only queues nothing (every candidate goes to the
+        // region), so there it is the positions the tail had to walk
+        if (kRounds && t.spill_total && sn && lane == 0) atomicAdd(t.spill_total, (unsigned long long)sn);
         // every placeholder and spill store of this wave complete before
         // its walks patch or read them
         __builtin_amdgcn_s_waitcnt(0);
@@ -915,7 +919,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         } else if (V == 5) {
             rt_tail<OUTW, false, 6>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
         } else {
-            rt_tail<OUTW>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+            const uint32_t nwalk = rt_tail<OUTW>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+            if (!kRounds && t.spill_total && nwalk && lane == 0)
+                atomicAdd(t.spill_total, (unsigned long long)nwalk);
         }
     }
     // the (at most two) chunks that touch the stream start or the tail: one

@@ -50,8 +50,9 @@ enum Kind { KIND_RT = 1, KIND_AC = 2, KIND_AUTO = 3 };
 
 // KIND_AUTO holds both images and picks a kernel per launch: the RT kernel
 // reports how many candidates it spilled (its queue overflowed: dense deep
-// matches, where the AC-DFA kernel is faster -- DESIGN.md §4); when a
-// launch spilled more than AUTO_SPILL_FRAC of its positions, the next
+// matches, where the AC-DFA kernel is faster -- DESIGN.md §4; a count-only
+// launch, which queues nothing, reports the positions its tail walked); when
+// a launch reported more than AUTO_SPILL_FRAC of its positions, the next
 // AUTO_HOLD launches run the DFA kernel, then one runs RT again to
 // re-measure.  The spill count comes back asynchronously (pinned memory +
 // event): a launch never waits for it.  reset() (a new stream) clears it.

@@ -648,6 +648,31 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     assert kernels[0] == pm.KIND_RT and kernels[-1] == pm.KIND_AC, kernels
 
 
+def test_auto_count_only_follows_deep_walks():
+    """Count-only RT launches spill every candidate, so the auto kind's
+    signal there is the positions the tail walked: the shipped stream moves
+    it to the DFA, random ASCII keeps it on RT; the counts are exact."""
+    import torch
+    n = 16 << 20
+    s = torch.cuda.current_stream()
+    deep = torch.from_numpy(np.concatenate([_tiled_ship(n), np.zeros(64, np.uint8)])).cuda()
+    sparse = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    assert pm.load().pm_hip_gen_stream_device(sparse.data_ptr(), 0, n + 64, 5, 0, s.cuda_stream) == 0
+    ref = matcher("snort", "ac")
+    for text, want_kernel in ((sparse, pm.KIND_RT), (deep, pm.KIND_AC)):
+        want = torch.zeros(1, dtype=torch.int64, device="cuda")
+        ref.scan_device(text.data_ptr(), 0, 0, n, None, want.data_ptr(), s.cuda_stream)
+        m = matcher("snort", "auto")
+        kernels = []
+        for _ in range(3):
+            got = torch.zeros(1, dtype=torch.int64, device="cuda")
+            m.scan_device(text.data_ptr(), 0, 0, n, None, got.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            kernels.append(m.kernel_last)
+            assert int(got.item()) == int(want.item())
+        assert kernels[0] == pm.KIND_RT and kernels[-1] == want_kernel, kernels
+
+
 def test_auto_stays_on_rt_for_sparse_matches():
     import torch
     n = 16 << 20
