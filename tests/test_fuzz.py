@@ -105,4 +105,11 @@ def test_fuzz_gpu_all_kinds(tmp_path, seed):
         torch.cuda.synchronize()
         assert np.array_equal(m._codes[ids.cpu().numpy().view(np.uint32)], exp), (seed, kind, "scan_device")
         assert int(cnt.item()) == int((exp != 0).sum())
+        ids16 = torch.empty(len(text), dtype=torch.int16, device="cuda")
+        m.scan_device(dt.data_ptr(), 0, 0, len(text), ids16.data_ptr(), None, s, out_width=2)
+        cnt.zero_()
+        m.scan_device(dt.data_ptr(), 0, 0, len(text), None, cnt.data_ptr(), s)  # count only
+        torch.cuda.synchronize()
+        assert torch.equal(ids16.to(torch.int32) & 0xFFFF, ids), (seed, kind, "u16")
+        assert int(cnt.item()) == int((exp != 0).sum()), (seed, kind, "count only")
         m.free()
