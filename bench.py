@@ -46,7 +46,7 @@ def parse():
                    help="dense: u32 id per position; dense16: u16 id per position; count: match count only")
     p.add_argument("--kernel", default="rt", choices=["rt", "ac", "auto"],
                    help="rt: reverse-trie kernel; ac: the AC dense DFA; auto: both, picked per launch")
-    p.add_argument("--stream", default="ascii", choices=["ascii", "bytes", "ship"],
+    p.add_argument("--stream", default="ascii", choices=["ascii", "bytes", "ship", "lines"],
                    help="ascii / bytes: seeded synthetic (DESIGN.md §5); ship: the reference's shipped "
                         "dictionaries_generated.stream tiled to --bytes (adversarial: deep matches)")
     p.add_argument("--seed", type=int, default=1)
@@ -135,7 +135,7 @@ def main():
 
     # CPU leg first, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.stream != "ship":
+    if rank == 0 and world == 1 and not args.no_cpu and args.stream in ("ascii", "bytes"):
         cpu = cpu_baseline(args)
 
     import torch
@@ -169,7 +169,7 @@ def main():
     pos0 = 0  # context bytes before the rank's first position (split layout)
     gen_off = 0
     if args.layout == "split":
-        if args.stream == "ship":
+        if args.stream in ("ship", "lines"):
             raise SystemExit("--layout split needs a generated stream (ascii / bytes)")
         from patternmatching_amd.shard import shard_plan
         seed = args.seed  # one logical stream
@@ -182,6 +182,8 @@ def main():
         ship = torch.from_numpy(np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8))
         reps = (n + 64 + ship.numel() - 1) // ship.numel()
         text.copy_(ship.to("cuda").repeat(reps)[: n + 64])
+    elif args.stream == "lines":
+        m.gen_lines_device(text.data_ptr(), n + 64, seed, stream.cuda_stream)
     elif lib.pm_hip_gen_stream_device(text.data_ptr(), gen_off, pos0 + n + 64, seed,
                                       0 if args.stream == "ascii" else 1, stream.cuda_stream) != 0:
         raise RuntimeError(lib.pm_hip_last_error().decode())
@@ -279,10 +281,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": ("synthetic: seeded splitmix64 %s stream per GPU (DESIGN.md §5), generated in HBM; "
-                     "dictionaries from the reference" % args.stream) if args.stream != "ship" else
-                    "the reference's shipped Streams/dictionaries_generated.stream (10,240 B) tiled in HBM; "
-                    "dictionaries from the reference",
+            "data": {"ship": "the reference's shipped Streams/dictionaries_generated.stream (10,240 B) tiled in "
+                             "HBM; dictionaries from the reference",
+                     "lines": "synthetic deep-match stream: the dictionary's own patterns drawn at random "
+                              "(splitmix64 per 1 KiB block), '\\n' after each, generated in HBM (DESIGN.md §5)"}.get(
+                args.stream, "synthetic: seeded splitmix64 %s stream per GPU (DESIGN.md §5), generated in HBM; "
+                             "dictionaries from the reference" % args.stream),
             "config": {
                 "workload": f"{args.dict}.dict, {n} B {args.stream} stream per GPU, "
                             + {"dense": "dense u32 match id per position", "dense16": "dense u16 match id per position",

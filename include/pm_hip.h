@@ -124,6 +124,11 @@ uint32_t pm_hip_parent_gid(void* obj, uint32_t gid);
 int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
                              void* hip_stream);
 void pm_gen_stream_host(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode);
+/* The "lines" stream: 1 KiB blocks of the object's patterns
+ * drawn at random (splitmix64), each followed by '\n' -- dense deep matches
+ * without the period of a tiled file.  Device and host give the same bytes. */
+int pm_hip_gen_lines_device(void* obj, uint8_t* d_dst, uint64_t n, uint64_t seed, void* hip_stream);
+void pm_gen_lines_host(void* obj, uint8_t* dst, uint64_t n, uint64_t seed);
 
 uint32_t pm_hip_n_patterns(void* obj);
 uint32_t pm_hip_max_pattern_len(void* obj);
@@ -158,6 +163,9 @@ int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int
 void pm_hip_debug_dfa_shape(int lanes_per_cu);
 /* Timing sweeps only: the AC-DFA kernel's shortest segment (0 = default). */
 void pm_hip_debug_dfa_min_seg(int min_seg);
+/* Timing sweeps only: segments per lane of the output-coded AC-DFA kernel
+ * (1 or 2; 0 = default). */
+void pm_hip_debug_dfa_chains(int chains);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

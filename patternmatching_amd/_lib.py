@@ -95,6 +95,8 @@ SIGNATURES = {
     "pm_hip_gen_stream_device": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_int, c_vp]),
     "pm_gen_stream_host": (None, [c_u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
+    "pm_hip_gen_lines_device": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint64, c_vp]),
+    "pm_gen_lines_host": (None, [c_vp, c_u8p, ctypes.c_uint64, ctypes.c_uint64]),
     "pm_hip_n_patterns": (ctypes.c_uint32, [c_vp]),
     "pm_hip_max_pattern_len": (ctypes.c_uint32, [c_vp]),
     "pm_hip_gid_index": (ctypes.c_uint32, [c_vp, ctypes.c_uint32]),
@@ -109,6 +111,7 @@ SIGNATURES = {
                                                  c_vp, c_vp]),
     "pm_hip_debug_dfa_shape": (None, [ctypes.c_int]),
     "pm_hip_debug_dfa_min_seg": (None, [ctypes.c_int]),
+    "pm_hip_debug_dfa_chains": (None, [ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
     "pm_flat_build_cached": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int,

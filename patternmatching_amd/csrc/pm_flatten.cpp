@@ -372,6 +372,9 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
         // suffix link / output (mpac.c:179, :318)
         im.out[v] = v == 0 ? 0 : (t.gid[v] ? t.gid[v] : im.out[fail[v]]);
     }
+    // output-coded transitions (pm_flatten.h): target | code << 20
+    if (pm_dfa_coded(S))
+        for (uint32_t& x : im.next) x |= std::min(im.out[x], PM_DFA_ESC) << 20;
     return im;
 }
 
@@ -380,7 +383,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 7;                     // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 8;                     // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);
@@ -473,10 +476,13 @@ bool values_ok(const PmImages& im, int kind, size_t ngid) {
     for (uint32_t g = 1; g <= P; ++g)
         if (par[g] > P || dep[g] != 1 + dep[par[g]]) return false;
     if (kind == 2) {
-        for (uint32_t x : im.dfa.next)
-            if (x >= im.dfa.states) return false;
         for (uint32_t x : im.dfa.out)
             if (x > P) return false;
+        const bool coded = pm_dfa_coded(im.dfa.states);
+        for (uint32_t x : im.dfa.next) {
+            const uint32_t t = coded ? x & PM_DFA_STATE_MASK : x;
+            if (t >= im.dfa.states || (coded && (x >> 20) != std::min(im.dfa.out[t], PM_DFA_ESC))) return false;
+        }
         return true;
     }
     const RtImage& rt = im.rt;

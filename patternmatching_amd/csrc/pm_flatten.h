@@ -89,8 +89,16 @@ struct RtImage {
     }
 };
 
+// With fewer than 2^20 states (every reference dictionary: merged has
+// 716,744) a transition word also carries its target's output: target |
+// min(out[target], PM_DFA_ESC) << 20, so a DFA step is one gather and only
+// PM_DFA_ESC (gid >= 4095) needs out[].
+constexpr uint32_t PM_DFA_STATE_MASK = 0xFFFFFu;
+constexpr uint32_t PM_DFA_ESC = 4095u;
+inline bool pm_dfa_coded(uint32_t states) { return states <= PM_DFA_STATE_MASK; }
+
 struct DfaImage {
-    std::vector<uint32_t> next;  // states * 256
+    std::vector<uint32_t> next;  // states * 256 (output-coded when pm_dfa_coded(states))
     std::vector<uint32_t> out;   // states
     uint32_t states = 0;
     size_t bytes() const { return next.size() * 4 + out.size() * 4; }

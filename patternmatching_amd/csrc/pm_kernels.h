@@ -25,9 +25,10 @@ struct RtDev {
 int64_t pm_rt_spill_items(int64_t n, int num_cu);
 
 struct DfaDev {
-    const uint32_t* next;  // states * 256
+    const uint32_t* next;  // states * 256 (output-coded when coded, pm_flatten.h)
     const uint32_t* out;   // states
     int64_t warm;          // max pattern length - 1
+    int coded;             // pm_dfa_coded(states)
 };
 
 // Positions [pos0, pos0+n) of text; bytes back to stream_start are context.
@@ -44,6 +45,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 // launch shape of the DFA kernel (timing sweeps): lanes per CU; <= 0
 // restores the default
 void pm_dfa_set_shape(int lanes_per_cu);
+void pm_dfa_set_chains(int chains);
 void pm_dfa_set_min_seg(int min_seg);
 // counts[0..4] += success, partial, false_neg, false_pos, all_matches of algo
 // against real (n u32 gids each, 16-B aligned); parent/depth: PmParents.
@@ -54,3 +56,5 @@ hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n
 hipError_t pm_launch_pattern_counts(const uint32_t* real, int64_t n, const uint32_t* parent, uint32_t n_gids,
                                    unsigned long long* hist, int num_cu, hipStream_t s);
 hipError_t pm_launch_gen(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode, hipStream_t s);
+hipError_t pm_launch_gen_lines(uint8_t* dst, uint64_t n, const uint8_t* pats, const uint32_t* offs, uint32_t npats,
+                               uint64_t seed, hipStream_t s);

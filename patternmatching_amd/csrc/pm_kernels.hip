@@ -1003,6 +1003,102 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
     }
 }
 
+// Output-coded DFA (the image of a dictionary of < 2^20 states, pm_flatten.h):
+// the transition word carries its target's output as a 12-bit code next to
+// the 20-bit target state (4095 = look it up in out[]), so a step is one
+// gather; CH segments per lane advance in lock step (CH gathers in flight
+// per lane).  Escapes are looked up after each 16-step block, off the chain.
+constexpr uint32_t DFA_STATE_MASK = 0xFFFFFu;  // must match pm_flatten.h
+constexpr uint32_t DFA_ESC = 4095u;
+
+template <int OUTW, int CH>
+__global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
+                                                                int64_t pos0, int64_t n, void* __restrict__ out,
+                                                                unsigned long long* __restrict__ count,
+                                                                const uint32_t* __restrict__ nxt,
+                                                                const uint32_t* __restrict__ outt, int64_t warm,
+                                                                int64_t seg_len) {
+    const int64_t nseg = (n + seg_len - 1) / seg_len;
+    const int64_t lanes = (int64_t)gridDim.x * DFA_THREADS;
+    uint32_t cnt = 0;
+    for (int64_t sg0 = (int64_t)blockIdx.x * DFA_THREADS + threadIdx.x; sg0 < nseg; sg0 += CH * lanes) {
+        int64_t lo[CH], hi[CH];
+        uint32_t s[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int64_t sg = sg0 + k * lanes;
+            lo[k] = sg < nseg ? pos0 + sg * seg_len : pos0 + n;
+            hi[k] = sg < nseg ? (lo[k] + seg_len < pos0 + n ? lo[k] + seg_len : pos0 + n) : pos0 + n;
+            int64_t wlo = lo[k] - warm;
+            if (wlo < stream_start) wlo = stream_start;
+            s[k] = 0;
+            if (sg < nseg)
+                for (int64_t i = wlo; i < lo[k]; ++i) s[k] = nxt[(size_t)s[k] * 256 + text[i]] & DFA_STATE_MASK;
+        }
+        const int64_t nblk = seg_len / 16;
+        for (int64_t b = 0; b < nblk; ++b) {
+            bool act[CH];
+            uint32_t W[CH][4];
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                act[k] = lo[k] + 16 * b + 16 <= hi[k];
+                any |= act[k];
+                const uint4 w = act[k] ? *reinterpret_cast<const uint4*>(text + lo[k] + 16 * b) : make_uint4(0, 0, 0, 0);
+                W[k][0] = w.x; W[k][1] = w.y; W[k][2] = w.z; W[k][3] = w.w;
+            }
+            if (!any) break;
+            uint32_t code[CH][16], st[CH][16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const uint32_t c = (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                    const uint32_t v = act[k] ? nxt[(size_t)s[k] * 256 + c] : 0u;
+                    s[k] = act[k] ? v & DFA_STATE_MASK : s[k];
+                    code[k][j] = v >> 20;
+                    st[k][j] = s[k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                if (!act[k]) continue;
+                uint32_t r[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) r[j] = code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                const int64_t i = lo[k] + 16 * b;
+                if (OUTW == 4) {
+                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
+                    o[0] = make_uint4(r[0], r[1], r[2], r[3]);
+                    o[1] = make_uint4(r[4], r[5], r[6], r[7]);
+                    o[2] = make_uint4(r[8], r[9], r[10], r[11]);
+                    o[3] = make_uint4(r[12], r[13], r[14], r[15]);
+                }
+                if (OUTW == 2) {
+                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + (i - pos0));
+                    o[0] = make_uint4(r[0] | r[1] << 16, r[2] | r[3] << 16, r[4] | r[5] << 16, r[6] | r[7] << 16);
+                    o[1] = make_uint4(r[8] | r[9] << 16, r[10] | r[11] << 16, r[12] | r[13] << 16, r[14] | r[15] << 16);
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) cnt += r[j] != 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            for (int64_t i = lo[k] + 16 * ((hi[k] - lo[k]) / 16); i < hi[k]; ++i) {
+                s[k] = nxt[(size_t)s[k] * 256 + text[i]] & DFA_STATE_MASK;
+                const uint32_t v = outt[s[k]];
+                if (OUTW) put_id<OUTW>(out, i - pos0, v);
+                cnt += v != 0u;
+            }
+        }
+    }
+    if (count) {
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
+    }
+}
+
 // Accuracy of one id stream against a reference one (Core/src/measure.c:
 // 174-190 with is_pattern_suffix, PatternsTree.c:485-494), one position per
 // lane-element: equal -> success; algo on real's parent chain -> partial;
@@ -1124,6 +1220,16 @@ __global__ __launch_bounds__(HIST_THREADS) void hist_kernel(const uint32_t* __re
         if (s_h[k]) atomicAdd(hist + lo + k, (unsigned long long)s_h[k]);
 }
 
+__global__ void gen_lines_kernel(uint8_t* __restrict__ dst, uint64_t n, const uint8_t* __restrict__ pats,
+                                 const uint32_t* __restrict__ offs, uint32_t npats, uint64_t seed) {
+    const uint64_t nb = (n + PM_LINES_BLOCK - 1) / PM_LINES_BLOCK;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += stride) {
+        const uint64_t lo = b * PM_LINES_BLOCK;
+        pm_lines_block(dst + lo, n - lo < PM_LINES_BLOCK ? n - lo : PM_LINES_BLOCK, b, pats, offs, npats, seed);
+    }
+}
+
 __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint64_t n, uint64_t seed, int mode) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
@@ -1224,22 +1330,40 @@ static int g_dfa_lanes_per_cu = DFA_LANES_PER_CU;
 // 16 MiB 0.76-0.86 -> 0.28-0.37, 64 MiB 1.06-1.43 -> 0.59-0.73; from 256
 // MiB up the lane cap decides and nothing changes.
 static int64_t g_dfa_min_seg = 0;  // pm_dfa_set_min_seg override (timing sweeps)
+// segments per lane of the output-coded kernel (profiles/r02/dfa_coded_ab.txt:
+// two chains at 512 lanes per CU beat the uncoded kernel on random ASCII,
+// the tiled shipped stream and the lines stream; one chain lost on the
+// shipped stream)
+constexpr int DFA_CHAINS = 2;
+static int g_dfa_chains = DFA_CHAINS;
 
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (!out) outw = 0;
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
-    // one segment per lane, none shorter than short_seg (above)
+    // one segment per lane and chain, none shorter than short_seg (above)
+    const int64_t ch = t.coded ? g_dfa_chains : 1;
     const int64_t lanes = (int64_t)num_cu * g_dfa_lanes_per_cu;
-    int64_t seg = (n + lanes - 1) / lanes;
+    int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
     seg = (seg + 15) & ~(int64_t)15;
     const int64_t nseg = (n + seg - 1) / seg;
-    int64_t blocks = (nseg + DFA_THREADS - 1) / DFA_THREADS;
+    int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), b(DFA_THREADS);
+    if (t.coded) {
+#define DC(W, C) \
+    hipLaunchKernelGGL((dfa_coded_kernel<W, C>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, t.out, t.warm, seg)
+        if (ch == 2) {
+            if (outw == 4) DC(4, 2); else if (outw == 2) DC(2, 2); else DC(0, 2);
+        } else {
+            if (outw == 4) DC(4, 1); else if (outw == 2) DC(2, 1); else DC(0, 1);
+        }
+#undef DC
+        return hipGetLastError();
+    }
     if (outw == 4)
         hipLaunchKernelGGL(dfa_scan_kernel<4>, g, b, 0, s, text, stream_start, pos0, n, out, count, t, seg);
     else if (outw == 2)
@@ -1251,6 +1375,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 
 void pm_dfa_set_shape(int lanes_per_cu) { g_dfa_lanes_per_cu = lanes_per_cu > 0 ? lanes_per_cu : DFA_LANES_PER_CU; }
 void pm_dfa_set_min_seg(int min_seg) { g_dfa_min_seg = min_seg >= 16 ? min_seg : 0; }
+void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : DFA_CHAINS; }
 
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,
                           const uint32_t* depth, unsigned long long* counts, int num_cu, hipStream_t s) {
@@ -1277,6 +1402,17 @@ hipError_t pm_launch_pattern_counts(const uint32_t* real, int64_t n, const uint3
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t pm_launch_gen_lines(uint8_t* dst, uint64_t n, const uint8_t* pats, const uint32_t* offs, uint32_t npats,
+                               uint64_t seed, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (npats == 0) return hipErrorInvalidValue;
+    const uint64_t nb = (n + PM_LINES_BLOCK - 1) / PM_LINES_BLOCK;
+    uint64_t blocks = (nb + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(gen_lines_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, n, pats, offs, npats, seed);
+    return hipGetLastError();
 }
 
 hipError_t pm_launch_gen(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode, hipStream_t s) {

@@ -130,6 +130,11 @@ struct PmHip {
     PipeSlot slot[2];
     double dev_seconds = 0.0;
     AutoPick pick;        // scan_device launches (read_block slots have their own)
+    // the lines stream generator's copy of the patterns (pm_hip_gen_lines_*)
+    std::vector<uint8_t> lines_pats;
+    std::vector<uint32_t> lines_offs;
+    uint8_t* d_lines_pats = nullptr;
+    uint32_t* d_lines_offs = nullptr;
     int last_kernel = 0;  // KIND_RT / KIND_AC of the last launch
 };
 
@@ -449,6 +454,7 @@ void pm_hip_compile(void* obj) {
         o->dfa.next = (const uint32_t*)dalloc_copy(o, im.dfa.next.data(), im.dfa.next.size() * 4);
         o->dfa.out = (const uint32_t*)dalloc_copy(o, im.dfa.out.data(), im.dfa.out.size() * 4);
         o->dfa.warm = o->max_len ? (int64_t)o->max_len - 1 : 0;
+        o->dfa.coded = pm_dfa_coded(im.dfa.states) ? 1 : 0;
     }
     o->d_parent = (const uint32_t*)dalloc_copy(o, im.par.parent.data(), im.par.parent.size() * 4);
     o->d_depth = (const uint32_t*)dalloc_copy(o, im.par.depth.data(), im.par.depth.size() * 4);
@@ -502,6 +508,8 @@ void pm_hip_free(void* obj) {
     (void)hipSetDevice(o->device);
     for (void* p : o->allocs) (void)hipFree(p);
     if (o->spill) (void)hipFree(o->spill);
+    if (o->d_lines_pats) (void)hipFree(o->d_lines_pats);
+    if (o->d_lines_offs) (void)hipFree(o->d_lines_offs);
     free_pick(o->pick);
     for (PipeSlot& q : o->slot) {
         free_slot(q);
@@ -627,6 +635,8 @@ int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int
     return e == hipSuccess ? 0 : -3;
 }
 
+void pm_hip_debug_dfa_chains(int chains) { pm_dfa_set_chains(chains); }
+
 void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }
 void pm_hip_debug_dfa_min_seg(int min_seg) { pm_dfa_set_min_seg(min_seg); }
 
@@ -638,6 +648,48 @@ int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64
         return -3;
     }
     return 0;
+}
+
+static void lines_table(PmHip* o) {
+    if (!o->lines_offs.empty()) return;
+    o->lines_offs.push_back(0);
+    for (const std::string& p : o->pats) {
+        o->lines_pats.insert(o->lines_pats.end(), p.begin(), p.end());
+        o->lines_offs.push_back((uint32_t)o->lines_pats.size());
+    }
+    if (o->lines_pats.empty()) o->lines_pats.push_back(0);
+}
+
+int pm_hip_gen_lines_device(void* obj, uint8_t* d_dst, uint64_t n, uint64_t seed, void* hip_stream) {
+    PmHip* o = as(obj);
+    if (o->pats.empty()) {
+        std::snprintf(g_err, sizeof(g_err), "gen_lines: no patterns");
+        return -2;
+    }
+    lines_table(o);
+    if (!o->d_lines_pats) {
+        PM_CHECK(hipMalloc(&o->d_lines_pats, o->lines_pats.size()));
+        PM_CHECK(hipMalloc(&o->d_lines_offs, o->lines_offs.size() * sizeof(uint32_t)));
+        PM_CHECK(hipMemcpy(o->d_lines_pats, o->lines_pats.data(), o->lines_pats.size(), hipMemcpyHostToDevice));
+        PM_CHECK(hipMemcpy(o->d_lines_offs, o->lines_offs.data(), o->lines_offs.size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice));
+    }
+    hipError_t e = pm_launch_gen_lines(d_dst, n, o->d_lines_pats, o->d_lines_offs, (uint32_t)o->pats.size(), seed,
+                                       (hipStream_t)hip_stream);
+    if (e != hipSuccess) {
+        std::snprintf(g_err, sizeof(g_err), "gen_lines: %s", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
+}
+
+void pm_gen_lines_host(void* obj, uint8_t* dst, uint64_t n, uint64_t seed) {
+    PmHip* o = as(obj);
+    if (o->pats.empty()) return;
+    lines_table(o);
+    for (uint64_t lo = 0, b = 0; lo < n; lo += PM_LINES_BLOCK, ++b)
+        pm_lines_block(dst + lo, n - lo < PM_LINES_BLOCK ? n - lo : PM_LINES_BLOCK, b, o->lines_pats.data(),
+                       o->lines_offs.data(), (uint32_t)o->pats.size(), seed);
 }
 
 void pm_gen_stream_host(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode) {

@@ -189,6 +189,19 @@ class HipMatcher:
         if rc != 0:
             raise RuntimeError(self.lib.pm_hip_last_error().decode())
 
+    def gen_lines_device(self, d_dst_ptr, n, seed, stream_ptr):
+        """pm_hip_gen_lines_device: the lines stream (random dictionary
+        patterns back to back, '\\n' after each) of this object's patterns."""
+        rc = self.lib.pm_hip_gen_lines_device(self.obj, d_dst_ptr, n, seed, stream_ptr)
+        if rc != 0:
+            raise RuntimeError(self.lib.pm_hip_last_error().decode())
+
+    def gen_lines(self, n, seed) -> np.ndarray:
+        """The same bytes on the host (pm_gen_lines_host)."""
+        buf = np.empty(n, np.uint8)
+        self.lib.pm_gen_lines_host(self.obj, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), n, seed)
+        return buf
+
     def score_device(self, d_algo_ptr, d_real_ptr, n, d_counts_ptr, stream_ptr):
         """pm_hip_score_device: d_counts (5 u64) += success, partial,
         false_neg, false_pos, all_matches of algo ids against real ids."""

@@ -16,7 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--dict", default="snort")
 ap.add_argument("--bytes", type=int, default=1 << 30)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--stream", type=int, default=0, help="0 ascii, 1 bytes, 2 the shipped stream tiled")
+ap.add_argument("--stream", type=int, default=0, help="0 ascii, 1 bytes, 2 the shipped stream tiled, 3 lines")
 ap.add_argument("--variants", default="0,1,2")
 ap.add_argument("--modes", default="dense,dense16,count")
 ap.add_argument("--exact", default="", help="variants whose dense u32 ids must equal v0's (checked after timing)")
@@ -32,7 +32,9 @@ m.compile()
 n = args.bytes
 s = torch.cuda.current_stream()
 text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-if args.stream == 2:
+if args.stream == 3:
+    m.gen_lines_device(text.data_ptr(), n + 64, 1, s.cuda_stream)
+elif args.stream == 2:
     import numpy as np
     ship = torch.from_numpy(np.fromfile(os.path.join(data, "dictionaries_generated.stream"), dtype=np.uint8))
     text.copy_(ship.cuda().repeat((n + 64) // ship.numel() + 1)[: n + 64])

@@ -9,11 +9,12 @@
 //     loaded images must equal the built ones);
 //   * walks the RT image the way pm_kernels.hip's rt_one / rt_from_d2 /
 //     rt_deep do, every access bounds-checked (.at()), and the DFA image the
-//     way dfa_scan_kernel does, and requires the two answers to agree at
+//     way dfa_scan_kernel / dfa_coded_kernel do, and requires the two answers to agree at
 //     every position of the stream given plus a synthetic tail;
 //   * checks the filters have no false negatives (a depth-3 node passes
 //     stage 1; a position answered below depth 2 passes stage 2).
 // Usage: host_check CACHE_DIR STREAM DICT...
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -238,9 +239,11 @@ int main(int argc, char** argv) {
     uint32_t s = 0;
     size_t nonnull = 0, deep = 0;
     for (int64_t i = 0; i < (int64_t)text.size(); ++i) {
-        s = dfa.next.at((size_t)s * 256 + text[i]);
+        const uint32_t x = dfa.next.at((size_t)s * 256 + text[i]);
+        s = pm_dfa_coded(dfa.states) ? x & PM_DFA_STATE_MASK : x;  // output-coded transitions
         CHECK(s < dfa.states, "state %u", s);
         const uint32_t want = dfa.out.at(s);
+        CHECK(!pm_dfa_coded(dfa.states) || (x >> 20) == std::min(want, PM_DFA_ESC), "code %u out %u", x >> 20, want);
         bool dp = false;
         uint32_t best2 = 0;
         const uint32_t got = rt_one(im, text, i, &dp, &best2);

@@ -164,13 +164,23 @@ def rt_scan(img, text, stream_start=0, use_filter=True):
 
 
 def dfa_scan(img, text):
+    """dfa_scan_kernel / dfa_coded_kernel: below 2^20 states a transition
+    word is target | min(out[target], 4095) << 20 (pm_flatten.h); the code
+    is checked against out[] at every step."""
     nxt = img.array("next")
     outt = img.array("out")
+    coded = len(outt) <= 0xFFFFF
     s = 0
     res = np.empty(len(text), np.uint32)
     for j, c in enumerate(np.asarray(text, dtype=np.uint8).tolist()):
-        s = int(nxt[s * 256 + c])
-        res[j] = outt[s]
+        x = int(nxt[s * 256 + c])
+        s = x & 0xFFFFF if coded else x
+        if coded:
+            code = x >> 20
+            assert code == min(int(outt[s]), 4095)
+            res[j] = code if code != 4095 else outt[s]
+        else:
+            res[j] = outt[s]
     return res
 
 

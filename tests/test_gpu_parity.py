@@ -553,6 +553,35 @@ def test_full_size_binary_and_deep_streams_kernels_agree(stream):
     torch.cuda.empty_cache()
 
 
+def test_lines_stream_generator_and_kernels():
+    """The lines stream (random dictionary patterns back to back): device
+    bytes == host bytes; on 64 MiB of it RT, AC and auto agree at every
+    position, and a window matches the oracle."""
+    import torch
+    n = 64 << 20
+    rt, ac, au = matcher("snort", "rt"), matcher("snort", "ac"), matcher("snort", "auto")
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    rt.gen_lines_device(dt.data_ptr(), n + 64, 3, s)
+    torch.cuda.synchronize()
+    host = rt.gen_lines(1 << 20, 3)
+    assert np.array_equal(dt[: 1 << 20].cpu().numpy(), host)
+    assert np.array_equal(ac.gen_lines(1 << 20, 3), host)  # the same patterns in the same order
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = torch.empty(n, dtype=torch.int32, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), None, s)
+    ac.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), None, s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert int((a != 0).sum().item()) > 0.9 * n  # deep: nearly every position inside a pattern
+    au.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), None, s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    o = oracle_for("snort")
+    o.reset()
+    assert np.array_equal(o.scan_codes(host), rt._codes[a[: 1 << 20].cpu().numpy().view(np.uint32)])
+
+
 def test_adversarial_stream_large_rt_equals_ac():
     """A 32 MiB tiling of the shipped adversarial stream queues far more
     positions than the worklist holds, so the scan kernel's in-kernel
