@@ -22,7 +22,9 @@ names = {"dense": "C3 snort 1 GiB dense_u32 (bench default, 16-core reference ba
          "ship": "snort, the shipped stream tiled to 1 GiB (deep matches), dense_u32",
          "ship_count": "snort, the shipped stream tiled to 1 GiB, count_only",
          "ship_ac": "snort, the shipped stream tiled to 1 GiB, AC dense DFA, dense_u32",
-         "ship_auto": "snort, the shipped stream tiled to 1 GiB, auto kind (RT, then AC after a spilling launch), dense_u32"}
+         "ship_auto": "snort, the shipped stream tiled to 1 GiB, auto kind (RT, then AC after a spilling launch), dense_u32",
+         "lines": "snort, the lines stream (random dictionary patterns, no period), 1 GiB, RT, dense_u32",
+         "lines_ac": "snort, the lines stream, 1 GiB, AC dense DFA (output-coded), dense_u32"}
 lines = {}
 for k, label in names.items():
     p = os.path.join(src, f"bench_{k}.json")

@@ -28,6 +28,8 @@ run ship --stream ship --no-cpu --steps 5
 run ship_count --stream ship --mode count --no-cpu --steps 5
 run ship_ac --stream ship --kernel ac --no-cpu --steps 5
 run ship_auto --stream ship --kernel auto --no-cpu --steps 5
+run lines --stream lines --no-cpu --steps 5
+run lines_ac --stream lines --kernel ac --no-cpu --steps 5
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
     python3 "$ROOT/bench.py" --no-cpu --steps 10 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail "$OUT/bench_prof.err"; exit 1; }
