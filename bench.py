@@ -261,6 +261,29 @@ def main():
     elapsed, kernel_ms = stats.tolist()
     total_matches = int(matches.item())
 
+    # the same kernel's streaming floor, live on this GPU: variant 2 of
+    # rt_scan_kernel runs the chunk loop's loads and stores with no lookups
+    # (its ids are not matches; `out` is not used after this)
+    floor = None
+    if rank == 0 and args.kernel == "rt" and pos0 == 0:
+        fts = []
+        for r in range(4):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            rc = lib.pm_hip_debug_scan_variant(m.obj, 2, text.data_ptr(), n, out_ptr, width, None, stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if rc != 0:
+                break
+            if r:
+                fts.append(e0.elapsed_time(e1))
+        if fts:
+            fms = sorted(fts)[len(fts) // 2]
+            floor = {"kernel_ms": round(fms, 4), "achieved": round(n * (1 + width) / (fms * 1e-3) / 1e9, 2),
+                     "kernel_over_floor": round(kernel_ms / fms, 4),
+                     "what": "rt_scan_kernel variant 2 on this GPU: the same loads and stores, no lookups "
+                             "(pm_hip_debug_scan_variant); kernel_over_floor = kernel_ms / floor kernel_ms"}
+
     if rank == 0:
         total_bytes = world * args.bytes * args.steps  # every rank scans --bytes positions
         value = total_bytes / elapsed / 1e9
@@ -316,6 +339,7 @@ def main():
                 "traffic": traffic,
                 "traffic_source": tr["source"] if tr else None,
                 "algorithmic_bytes_per_launch": n * alg_per_pos,
+                "streaming_floor": floor,
             },
             "cpu_baseline": cpu,
         }
