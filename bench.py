@@ -317,7 +317,8 @@ def main():
                 "dict": args.dict,
                 "stream_bytes_per_gpu": n,
                 "mode": args.mode,
-                "kernel": ("auto: RT or AC-DFA per launch by the RT spill rate (last launch: %s)"
+                "kernel": ("auto: RT, or the AC-DFA when a deep RT launch (spill > 10%%) is slower than a timed AC trial "
+                           "(last launch: %s)"
                            % {1: "RT", 2: "AC"}.get(m.kernel_last, "?") if args.kernel == "auto" else
                            {"rt": "reverse-suffix-trie walk", "ac": "Aho-Corasick dense DFA"}[args.kernel]),
                 "parallelism": (f"independent stream shards x{world}" if args.layout == "shards" else

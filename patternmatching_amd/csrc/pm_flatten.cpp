@@ -150,6 +150,8 @@ std::vector<uint32_t> derive_filters(const RtImage& im) {
             const uint32_t rk = R[0] >> 30;
             if (rk == RT_REC_KIDS) {
                 for (uint32_t j = 0; j < ((R[0] >> 24) & 63u) && j < RT_REC_INLINE; ++j) s4((R[2 + j / 4] >> (8 * (j & 3))) & 0xFFu);
+            } else if (rk == RT_REC_CHAIN) {
+                s4(R[3] >> 24);
             } else if (rk == RT_REC_WIDE && (size_t)(R[2] + 1) * RT_WIDE_WORDS <= im.wide.size()) {
                 const uint32_t* W = &im.wide[(size_t)R[2] * RT_WIDE_WORDS];
                 for (uint32_t c = 0; c < 256; ++c)
@@ -288,6 +290,18 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g) {
         R[1] = best[v];
         if (nch == 0) {
             R[0] = RT_REC_LEAF << 30;
+        } else if (nch == 1) {
+            // the run below v: consecutive one-child records, no pattern inside
+            uint32_t L = 1, w = t.cstart[v];
+            uint64_t P = (uint64_t)t.label[w] << 56;
+            while (L < RT_CHAIN_MAX && t.ccount[w] == 1 && t.cstart[w] == w + 1 && !t.gid[w]) {
+                P |= (uint64_t)t.label[w + 1] << (8 * (7 - L));
+                ++L;
+                ++w;
+            }
+            R[0] = (RT_REC_CHAIN << 30) | (L << 24) | first;
+            R[2] = (uint32_t)P;
+            R[3] = (uint32_t)(P >> 32);
         } else if (nch <= RT_REC_INLINE) {
             R[0] = (RT_REC_KIDS << 30) | (nch << 24) | first;
             for (uint32_t j = 0; j < nch; ++j) R[2 + j / 4] |= (uint32_t)t.label[t.cstart[v] + j] << (8 * (j & 3));
@@ -383,7 +397,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 8;                     // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 9;                     // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);
@@ -515,6 +529,18 @@ bool values_ok(const PmImages& im, int kind, size_t ngid) {
             if (cnt < 1 || cnt > RT_REC_INLINE || first <= n || (uint64_t)first + cnt > rt.nrec) return false;
             continue;
         }
+        if (rk == RT_REC_CHAIN) {
+            // the run the record describes is the one the records hold
+            if (cnt < 1 || cnt > RT_CHAIN_MAX || first <= n || (uint64_t)first + cnt > rt.nrec) return false;
+            const uint64_t Pb = (uint64_t)R[3] << 32 | R[2];
+            for (uint32_t k = 1; k < cnt; ++k) {
+                const uint32_t* C = &rt.rec[(size_t)(first + k - 1) * RT_REC_WORDS];
+                if (C[0] >> 30 != RT_REC_CHAIN || (C[0] & 0xFFFFFFu) != first + k || C[1] != R[1] ||
+                    (C[3] >> 24) != ((Pb >> (8 * (7 - k))) & 0xFFu))
+                    return false;
+            }
+            continue;
+        }
         if (rk != RT_REC_WIDE || R[2] >= rt.nwide || first <= n) return false;
         const uint32_t* W = &rt.wide[(size_t)R[2] * RT_WIDE_WORDS];
         uint64_t idx = first;
@@ -539,7 +565,7 @@ uint64_t pm_image_key(const std::vector<std::string>& pats, int kind) {
     // few keys): a change to either gives new keys, not a stale hit
     uint32_t lay[] = {RT_T1_BASE, RT_CONT16, RT_CONT32, (uint32_t)RT_REC_WORDS, RT_FILTER_WORDS, RT_F3_WORDS,
                       RT_F4_WORDS, RT_T3H_INLINE, RT_T3H_VALID, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                      RT_REC_INLINE, (uint32_t)RT_WIDE_WORDS, (uint32_t)PM_DFA_DFS_DEPTH};
+                      RT_REC_INLINE, (uint32_t)RT_WIDE_WORDS, (uint32_t)PM_DFA_DFS_DEPTH, RT_CHAIN_MAX};
     const uint32_t probe[2] = {0x00A1B2C3u, 0x00FFFFFFu};
     for (int q = 0; q < 2; ++q) {
         const uint32_t k = probe[q];

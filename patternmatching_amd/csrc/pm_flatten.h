@@ -143,7 +143,15 @@ constexpr uint32_t RT_T1_BASE = 65536;   // t12[65536 + c]: lookback of exactly 
 constexpr uint32_t RT_CONT16 = 0x8000u;  // t12: depth-2 node has children (low 15 bits: best so far)
 constexpr uint32_t RT_CONT32 = 0x80000000u;  // t3: continue at record (low 31 bits)
 constexpr int RT_REC_WORDS = 4;
-constexpr uint32_t RT_REC_LEAF = 0, RT_REC_KIDS = 1, RT_REC_WIDE = 3;  // record kinds (x >> 30)
+constexpr uint32_t RT_REC_LEAF = 0, RT_REC_KIDS = 1, RT_REC_CHAIN = 2, RT_REC_WIDE = 3;  // record kinds (x >> 30)
+// A one-child node's record is a CHAIN: x = kind | L << 24 | first, y = best,
+// and (w << 32 | z) holds the bytes b_0 .. b_{L-1} of its run at bytes 7 ..
+// 8-L (b_0, the child's byte, in the top byte of w).  The run: the child is
+// record `first`, and for k = 1 .. L-1 record first+k-1 has one child,
+// record first+k, reached by b_k, and no pattern ends at it.  A walk may
+// consume the m <= L leading bytes that match in one step: it is then at
+// record first+m-1, and if it stops there (m < L) the answer is y.
+constexpr uint32_t RT_CHAIN_MAX = 8;
 constexpr uint32_t RT_REC_INLINE = 8;  // children held inline in a record
 constexpr int RT_WIDE_WORDS = 16;
 // DFA state numbering: breadth-first to this depth, then children blocks in

@@ -56,7 +56,7 @@ constexpr uint32_t CONT32 = 0x80000000u;
 constexpr uint32_t T3H_VALID = 1u << 24;
 constexpr uint32_t RT_POSMASK = (1u << 30) - 1;  // queue item: position - pos0
 constexpr uint32_t RT_SLOT2 = 1u << 30;          // queue item: probe t3h slot2
-constexpr uint32_t RT_REC_LEAF_K = 0, RT_REC_KIDS_K = 1, RT_REC_WIDE_K = 3;  // record kinds, must match pm_flatten.h
+constexpr uint32_t RT_REC_LEAF_K = 0, RT_REC_KIDS_K = 1, RT_REC_CHAIN_K = 2, RT_REC_WIDE_K = 3;  // record kinds, must match pm_flatten.h
 
 __device__ __forceinline__ uint32_t rt_hash(uint32_t k) { return k * 0x9E3779B1u; }  // pm_rt_hash
 // pm_rt_fhash of the low 24 bits of k (the operand's top byte is ignored):
@@ -153,7 +153,10 @@ __device__ __forceinline__ uint32_t rt_deep(const uint8_t* __restrict__ text, co
         const uint32_t c = text[i - d];
         const uint32_t kind = rec_kind(R), first = R.x & 0xFFFFFFu;
         if (kind == RT_REC_LEAF_K) return R.y;
-        if (kind == RT_REC_KIDS_K) {
+        if (kind == RT_REC_CHAIN_K) {  // one step of the run: its first byte
+            if (c != (R.w >> 24)) return R.y;
+            node = first;
+        } else if (kind == RT_REC_KIDS_K) {
             const uint32_t j = rec_kid_index(R, c);
             if (j == ((R.x >> 24) & 63u)) return R.y;
             node = first + j;
@@ -402,6 +405,18 @@ __device__ __forceinline__ uint32_t rt_tail(const uint8_t* __restrict__ text, in
             const bool rend = z.dd >= z.av;
             const bool rnext = !rend && rkind == RT_REC_KIDS_K && jr != ((A.x >> 24) & 63u);
             const bool rwide = !rend && rkind == RT_REC_WIDE_K;
+            // TS_REC at a CHAIN record: the run's bytes against text[i-d],
+            // text[i-d-1], ... as far as the cached window, the run and the
+            // stream allow, in one step (window byte ro to the top byte, then
+            // the leading equal bytes of the two 64-bit words)
+            const uint64_t win = ((uint64_t)rhi << 32 | rlo) << (8 * (7 - ro));
+            const uint64_t dif = win ^ ((uint64_t)A.w << 32 | A.z);
+            const uint32_t meq = dif ? (uint32_t)__builtin_clzll(dif) >> 3 : 8u;
+            const uint32_t clen = (A.x >> 24) & 63u;
+            const uint32_t cav = z.av > z.dd ? z.av - z.dd : 0u;
+            const uint32_t clim = min(min(clen, ro + 1u), cav);
+            const uint32_t cm = min(meq, clim);
+            const bool cnext = rkind == RT_REC_CHAIN_K && cm >= 1u && (cm == clen || (cm == ro + 1u && cm < cav));
             // TS_WIDE: A is the quarter of the wide entry holding byte c
             const uint32_t wnode = wide_child(A, z.c);
             const bool wnext = wnode != ~0u;
@@ -419,14 +434,14 @@ __device__ __forceinline__ uint32_t rt_tail(const uint8_t* __restrict__ text, in
                 z.twa = INT32_MIN / 2;  // nothing cached
             }
             if (st == TS_REC) {
-                nst = rnext ? TS_REC : rwide ? TS_WIDE : TS_EMPTY;
-                fin = !rnext && !rwide;
+                nst = (rnext || cnext) ? TS_REC : rwide ? TS_WIDE : TS_EMPTY;
+                fin = !rnext && !rwide && !cnext;
                 ans = A.y;
                 z.tlo = rlo;
                 z.thi = rhi;
                 z.twa = rta;
-                z.node = first + jr;
-                z.dd += rnext ? 1u : 0u;
+                z.node = cnext ? first + cm - 1u : first + jr;
+                z.dd += rnext ? 1u : cnext ? cm : 0u;
                 z.c = c;
             }
             if (st == TS_WIDE) {
@@ -667,7 +682,13 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 v = R.y;
                 if ((int64_t)d < avail) {
                     const uint32_t kind = rec_kind(R);
-                    if (kind == RT_REC_KIDS_K) {
+                    if (kind == RT_REC_CHAIN_K) {  // one step of the run (the tail takes several)
+                        if (tc == (R.w >> 24)) {
+                            node = R.x & 0xFFFFFFu;
+                            ++d;
+                            again = true;
+                        }
+                    } else if (kind == RT_REC_KIDS_K) {
                         const uint32_t j = rec_kid_index(R, tc);
                         if (j != ((R.x >> 24) & 63u)) {
                             node = (R.x & 0xFFFFFFu) + j;

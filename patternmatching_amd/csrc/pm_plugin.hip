@@ -50,23 +50,33 @@ enum Kind { KIND_RT = 1, KIND_AC = 2, KIND_AUTO = 3 };
 
 // KIND_AUTO holds both images and picks a kernel per launch: the RT kernel
 // reports how many candidates it spilled (its queue overflowed: dense deep
-// matches, where the AC-DFA kernel is faster -- DESIGN.md §4; a count-only
-// launch, which queues nothing, reports the positions its tail walked); when
-// a launch reported more than AUTO_SPILL_FRAC of its positions, the next
-// AUTO_HOLD launches run the DFA kernel, then one runs RT again to
-// re-measure.  The spill count comes back asynchronously (pinned memory +
-// event): a launch never waits for it.  reset() (a new stream) clears it.
+// matches -- DESIGN.md §4; a count-only launch, which queues nothing,
+// reports the positions its tail walked) and its time; when a launch
+// reported more than AUTO_SPILL_FRAC of its positions, the next AUTO_TRIAL
+// launches run the AC-DFA kernel, the last one timed (the first pays cold
+// caches), and whichever of the two took less per position
+// runs the next AUTO_HOLD launches; then RT measures again.  (Deep input is
+// where the DFA can win: on the tiled shipped stream it is 2.2x RT, on the
+// non-periodic lines stream RT is 1.4x the DFA.)  Counts and times come back
+// through pinned memory and events, waited for at the next launch (see
+// launch()).  reset() (a new stream) clears it.
 constexpr double AUTO_SPILL_FRAC = 0.10;
+constexpr int AUTO_TRIAL = 2;
 constexpr int AUTO_HOLD = 64;
 
 struct AutoPick {
-    unsigned long long* d_spill = nullptr;  // device counter of the last RT launch
+    unsigned long long* d_spill = nullptr;  // device counter of the last measured RT launch
     unsigned long long* h_spill = nullptr;  // pinned copy
-    hipEvent_t ev = nullptr;
-    bool pending = false;
-    int64_t n_last = 0;
-    int dfa_left = 0;
-    int last = 0;  // kernel of the last launch (KIND_RT / KIND_AC)
+    hipEvent_t ev = nullptr;                // the copy has landed
+    hipEvent_t rt0 = nullptr, rt1 = nullptr, ac0 = nullptr, ac1 = nullptr;  // timing of the measured launches
+    bool pending = false;     // a measured RT launch (spill count + time) in flight
+    bool ac_pending = false;  // a timed AC trial launch in flight
+    int trial = 0;            // AC trial launches left (the last one is timed)
+    int64_t n_last = 0, n_ac = 0;
+    double rt_ns = 0.0;       // the measured RT launch's ns per position
+    int dfa_left = 0;         // launches left on the chosen kernel (hold)
+    int chosen = 0;           // KIND_RT / KIND_AC during a hold
+    int last = 0;             // kernel of the last launch (KIND_RT / KIND_AC)
 };
 
 // read_block pipeline blocks (positions): the upload, kernel and download of
@@ -141,7 +151,8 @@ struct PmHip {
 void free_pick(AutoPick& a) {
     if (a.d_spill) (void)hipFree(a.d_spill);
     if (a.h_spill) (void)hipHostFree(a.h_spill);
-    if (a.ev) (void)hipEventDestroy(a.ev);
+    for (hipEvent_t e : {a.ev, a.rt0, a.rt1, a.ac0, a.ac1})
+        if (e) (void)hipEventDestroy(e);
     a = AutoPick();
 }
 
@@ -253,31 +264,66 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
     t.spill_cap = spill_cap;
     if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
     if (o->kind == KIND_AC) return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
-    // KIND_AUTO
+    // KIND_AUTO (see AUTO_SPILL_FRAC): RT launches are measured (spill
+    // count and time); a deep one triggers one timed AC trial; the faster
+    // per position then runs AUTO_HOLD launches.  Results are read only once
+    // their events have completed, so no launch waits.
     if (!ap.ev) {
         PM_CHECK(hipMalloc(&ap.d_spill, sizeof(unsigned long long)));
         PM_CHECK(hipHostMalloc(&ap.h_spill, sizeof(unsigned long long), hipHostMallocDefault));
         PM_CHECK(hipEventCreateWithFlags(&ap.ev, hipEventDisableTiming));
+        for (hipEvent_t* e : {&ap.rt0, &ap.rt1, &ap.ac0, &ap.ac1}) PM_CHECK(hipEventCreate(e));
     }
-    if (ap.pending && hipEventQuery(ap.ev) == hipSuccess) {
+    // measurements are waited for (not polled): a burst of device-side
+    // launches would otherwise outrun them and never adapt; the wait is one
+    // host-side bubble per measurement, i.e. per AUTO_HOLD + AUTO_TRIAL + 1
+    // launches, and free in the read_block pipeline, which has synchronized
+    // the slot already
+    if (ap.pending && hipEventSynchronize(ap.ev) == hipSuccess) {
         ap.pending = false;
-        if ((double)*ap.h_spill > AUTO_SPILL_FRAC * (double)ap.n_last) ap.dfa_left = AUTO_HOLD;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ap.rt0, ap.rt1) == hipSuccess) ap.rt_ns = ms * 1e6 / (double)ap.n_last;
+        if ((double)*ap.h_spill > AUTO_SPILL_FRAC * (double)ap.n_last) {
+            ap.trial = AUTO_TRIAL;
+        } else {  // shallow: RT holds
+            ap.chosen = KIND_RT;
+            ap.dfa_left = AUTO_HOLD;
+        }
     }
-    if (ap.dfa_left > 0) {
+    if (ap.ac_pending && hipEventSynchronize(ap.ac1) == hipSuccess) {
+        ap.ac_pending = false;
+        float ms = 0.f;
+        const double ac_ns = hipEventElapsedTime(&ms, ap.ac0, ap.ac1) == hipSuccess ? ms * 1e6 / (double)ap.n_ac : 0.0;
+        ap.chosen = ac_ns > 0.0 && ac_ns < ap.rt_ns ? KIND_AC : KIND_RT;
+        ap.dfa_left = AUTO_HOLD;
+    }
+    hipError_t e = hipSuccess;
+    if (ap.dfa_left > 0) {  // hold the chosen kernel
         --ap.dfa_left;
+        ap.last = ap.chosen;
+        if (ap.chosen == KIND_AC) return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+        return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
+    }
+    if (ap.trial > 0 && !ap.ac_pending) {  // AC trial launches; the last one is timed (the first pays cold caches)
         ap.last = KIND_AC;
-        return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+        if (--ap.trial > 0) return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+        e = hipEventRecord(ap.ac0, s);
+        if (e == hipSuccess) e = pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+        if (e == hipSuccess) e = hipEventRecord(ap.ac1, s);
+        ap.ac_pending = e == hipSuccess;
+        ap.n_ac = n;
+        return e;
     }
     ap.last = KIND_RT;
     t.spill_total = ap.d_spill;
-    hipError_t e = hipMemsetAsync(ap.d_spill, 0, sizeof(unsigned long long), s);
+    e = hipMemsetAsync(ap.d_spill, 0, sizeof(unsigned long long), s);
+    if (e == hipSuccess) e = hipEventRecord(ap.rt0, s);
     if (e == hipSuccess) e = pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
-    if (e == hipSuccess && !ap.pending) {
-        e = hipMemcpyAsync(ap.h_spill, ap.d_spill, sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipEventRecord(ap.ev, s);
-        ap.pending = e == hipSuccess;
-        ap.n_last = n;
-    }
+    if (e == hipSuccess) e = hipEventRecord(ap.rt1, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(ap.h_spill, ap.d_spill, sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(ap.ev, s);
+    ap.pending = e == hipSuccess;
+    ap.n_last = n;
     return e;
 }
 
@@ -496,7 +542,9 @@ void pm_hip_reset(void* obj) {
     // belongs to the old stream: wait for it and drop it)
     auto forget = [](AutoPick& a) {
         if (a.pending) (void)hipEventSynchronize(a.ev);
-        a.pending = false;
+        if (a.ac_pending) (void)hipEventSynchronize(a.ac1);
+        a.pending = a.ac_pending = false;
+        a.trial = 0;
         a.dfa_left = 0;
     };
     forget(o->pick);

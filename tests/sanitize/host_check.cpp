@@ -60,7 +60,22 @@ uint32_t rt_deep(const RtImage& im, const std::vector<uint8_t>& text, uint32_t n
         const uint32_t c = text.at(i - d);
         if (kind == RT_REC_LEAF) return best;
         uint32_t next = 0;
-        if (kind == RT_REC_KIDS) {
+        if (kind == RT_REC_CHAIN) {
+            // the whole run at once, as the device tail does (pm_flatten.h)
+            const uint64_t P = (uint64_t)im.rec.at(R + 3) << 32 | im.rec.at(R + 2);
+            uint32_t m = 0;
+            while (m < cnt && d + m < avail && text.at(i - d - m) == ((P >> (8 * (7 - m))) & 0xFFu)) ++m;
+            if (m == 0) return best;
+            if (m < cnt) {  // stopped inside the run: no pattern there, the answer is this record's
+                const size_t Rm = (size_t)(first + m - 1) * RT_REC_WORDS;
+                CHECK(im.rec.at(Rm + 1) == best, "chain best %u vs %u", im.rec.at(Rm + 1), best);
+                return best;
+            }
+            CHECK(first + m - 1 > node && first + m - 1 < im.nrec, "chain %u -> %u", node, first + m - 1);
+            node = first + m - 1;
+            d += m;
+            continue;
+        } else if (kind == RT_REC_KIDS) {
             uint32_t j = 0;
             while (j < cnt && ((im.rec.at(R + 2 + j / 4) >> (8 * (j & 3))) & 0xFFu) != c) ++j;
             if (j == cnt) return best;

@@ -91,8 +91,9 @@ def t3h_lookup(t3h, bits, key24):
 
 
 def rec_walk(rec, wide, text, p, avail, node, d):
-    """16-B node records (pm_flatten.h): leaf / up to 8 inline children /
-    wide (4 quarters {word 2q, word 2q+1, first child index, best})."""
+    """16-B node records (pm_flatten.h): leaf / one child and its run (chain)
+    / up to 8 inline children / wide (4 quarters {word 2q, word 2q+1, first
+    child index, best})."""
     while True:
         x, best, z, w = (int(v) for v in rec[node])
         if d >= avail:
@@ -101,6 +102,15 @@ def rec_walk(rec, wide, text, p, avail, node, d):
         c = int(text[p - d])
         if kind == 0:
             return best
+        if kind == 2:  # chain: the run's bytes at once (pm_flatten.h)
+            P = (w << 32) | z
+            m = 0
+            while m < cnt and d + m < avail and int(text[p - d - m]) == (P >> (8 * (7 - m))) & 0xFF:
+                m += 1
+            if m < cnt:
+                return best  # stopped inside the run (or before it): no pattern there
+            node, d = first + m - 1, d + m
+            continue
         if kind == 1:
             kids = [((z | (w << 32)) >> (8 * j)) & 0xFF for j in range(cnt)]
             if c not in kids:

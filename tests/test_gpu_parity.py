@@ -656,8 +656,9 @@ def _tiled_ship(n):
 
 def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     """The auto kind runs RT first; on the reference's shipped stream (dense
-    deep matches: the RT kernel spills > 10 % of positions) the next launches
-    run the AC-DFA kernel, and every launch is exact."""
+    deep matches: the RT kernel spills > 10 % of positions) the next launch
+    is a timed AC-DFA trial, then the faster of the two holds; every launch
+    is exact."""
     import torch
     n = 16 << 20
     text = _tiled_ship(n)
@@ -668,13 +669,15 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
     m = matcher("et", "auto")
     kernels = []
-    for _ in range(4):
+    for _ in range(5):
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
         kernels.append(m.kernel_last)
         assert torch.equal(got, want)
-    assert kernels[0] == pm.KIND_RT and kernels[-1] == pm.KIND_AC, kernels
+    # RT first (measured: it spills), then two AC trial launches (the second
+    # timed); the faster of the two per position holds after that
+    assert kernels[:3] == [pm.KIND_RT, pm.KIND_AC, pm.KIND_AC], kernels
 
 
 def test_auto_count_only_follows_deep_walks():
@@ -699,7 +702,8 @@ def test_auto_count_only_follows_deep_walks():
             torch.cuda.synchronize()
             kernels.append(m.kernel_last)
             assert int(got.item()) == int(want.item())
-        assert kernels[0] == pm.KIND_RT and kernels[-1] == want_kernel, kernels
+        # deep: the walks trigger one timed AC trial; sparse: RT throughout
+        assert kernels[0] == pm.KIND_RT and (pm.KIND_AC in kernels) == (want_kernel == pm.KIND_AC), kernels
 
 
 def test_auto_stays_on_rt_for_sparse_matches():
