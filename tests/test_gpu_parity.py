@@ -187,6 +187,10 @@ EDGE_DICTS = {
     "nested": [b"abcdef", b"cdef", b"ef", b"f", b"zzzzzzzzzz", b"zz"],
     "dense_short": [bytes([i]) for i in range(256)] + [bytes([i, j]) for i in range(0, 256, 7) for j in range(0, 256, 5)],
     "long": [bytes(range(40, 240)), bytes(range(40, 240))[100:], b"x" * 300, b"x" * 299 + b"y"],
+    # the RT image's limit (max_len <= 511, pm_flatten.cpp) and one past it
+    # (the RT and auto kinds then run the AC-DFA kernel alone)
+    "max_len_511": [b"ab" * 255 + b"a", b"ba" * 100, b"q"],
+    "max_len_600": [b"ab" * 300, b"ba" * 100, b"q"],
 }
 
 
@@ -201,6 +205,9 @@ def test_edge_dictionaries_brute_force(name, kind):
     rng = np.random.default_rng(9)
     alphabet = np.unique(np.frombuffer(b"".join(pats), np.uint8))
     text = rng.choice(alphabet, size=20000).astype(np.uint8)
+    if name.startswith("max_len"):
+        for k in range(2000, 18000, 1500):  # long alternating runs: the whole patterns occur
+            text[k:k + 700] = np.frombuffer(b"ab" * 350, np.uint8)
     if name == "long":
         text[5000:5200] = np.frombuffer(bytes(range(40, 240)), np.uint8)
         text[8000:8300] = ord("x")
