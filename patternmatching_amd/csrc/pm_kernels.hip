@@ -9,23 +9,31 @@
 //   warm-up.  Per position:
 //     depth <= 2   one u16 lookup in an LDS-resident 64K table keyed by the
 //                  last two bytes (t12);
-//     depth 3      only when t12 says the depth-2 node has children: a 2-bit
-//                  blocked Bloom filter in LDS over the 3-byte suffixes that
-//                  exist; a filter hit (about 1.5 % of positions on random
-//                  text, no false negatives) is queued;
-//     queue        per wave, filled with ballot/mbcnt prefix offsets and
-//                  drained by all 64 lanes at once: one probe of an
-//                  L2-resident hash table of depth-3 suffixes and, past depth
-//                  3, one 48-B bitmap-rank record per step.
+//     depth 3      only when t12 says the depth-2 node has children: a
+//                  3-bit blocked Bloom filter in LDS over the 3-byte
+//                  suffixes that exist (stage 1; ~1.9% of random-ASCII
+//                  positions pass, no false negatives), then a second LDS
+//                  filter over 3-byte patterns and 4-byte suffixes (stage 2);
+//     queue        per wave, filled with DPP prefix offsets and drained by
+//                  all 64 lanes at once: one probe of an L2-resident cuckoo
+//                  table of depth-3 suffixes and, past depth 3, one 16-B
+//                  node record per step;
+//     spill/tail   what the queue cannot hold goes to a per-wave region,
+//                  resolved after the chunk loop in two uniform phases
+//                  (batched probes, then lock-step walks that take a run of
+//                  one-child nodes per step from its chain record).
 //   Each lane owns four groups of four consecutive positions at stride 256,
 //   so every load instruction reads 256 contiguous bytes and every store
 //   instruction writes 1 KiB of contiguous match ids; the next chunk's bytes
 //   are loaded while the current one is resolved.
 //
-// dfa_scan_kernel the reference automaton itself, flattened to a dense DFA
-//   (next[s*256+c], out[s]); one lane per stream segment, started from the
-//   root max_len-1 bytes before the segment (SURVEY.md §0.1 shard rule), so
-//   every segment is independent and exact.
+// dfa_coded_kernel / dfa_scan_kernel  the reference automaton itself,
+//   flattened to a dense DFA whose transition words carry their target's
+//   output (next[s*256+c] = target | code << 20; the uncoded form for
+//   automata of 2^20 states or more); one lane per stream segment (two in
+//   lock step when coded), started from the root max_len-1 bytes before the
+//   segment (SURVEY.md §0.1 shard rule), so every segment is independent
+//   and exact.
 #include <type_traits>
 
 #include <algorithm>
