@@ -38,9 +38,13 @@
 //                                           contiguous);
 //                                           kind 2: RT_CONT32 | n3's record
 //             rec   u32x4[nrec]       16-B records for nodes of depth >= 3
-//                                     (BFS order, children contiguous):
+//                                     (BFS to depth 3, then depth-first
+//                                     child blocks; children contiguous):
 //                                       x = kind << 30 | count << 24 | first
 //                                           (kind RT_REC_LEAF: no children;
+//                                            RT_REC_CHAIN: one child, and
+//                                            count = the bytes of its run in
+//                                            z, w (below, RT_REC_CHAIN);
 //                                            RT_REC_KIDS: count <= 8 children,
 //                                            their bytes in z, w (byte j =
 //                                            child j, sorted), child j at
@@ -57,7 +61,9 @@
 //  DfaImage the Aho-Corasick automaton of Core/src/mpac.c (goto + BFS
 //           failure links + suffix/output links, :147-210) flattened into a
 //           dense DFA: next[s*256 + c] and out[s] (gid of the longest pattern
-//           that is a suffix of state s, 0 if none), states BFS-numbered.
+//           that is a suffix of state s, 0 if none), states BFS-numbered;
+//           below 2^20 states next also carries the target's output code
+//           (pm_dfa_coded, below).
 //
 // Pattern ids: gid 1..P, short patterns (length <= 2) first so that every
 // depth<=2 answer fits the 15-bit payload of a t12 entry.
