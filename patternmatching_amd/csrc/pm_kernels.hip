@@ -587,7 +587,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     struct Round {
         uint32_t n;     // items (wave-uniform)
         uint32_t keep;  // items that may survive the round (wave-uniform): ring room they hold
-        uint32_t fk, fp, tc;
+        uint32_t fk, fp;
+        u32x2 tw;       // record steps: the aligned 8 text bytes holding text[i-d]
         uint32_t skip;  // stage 2 rejected the item: its answer is the placeholder
         u32x4 L0;
     };
@@ -621,9 +622,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         const uint32_t slot = (r.fp & RT_SLOT2) ? rt_slot2(k, t.t3h_bits) : rt_slot1(k, t.t3h_bits);
         const u32x4* W = reinterpret_cast<const u32x4*>(t.wide) + (size_t)(r.fk & 0x3FFFu) * 4 + ((r.fk >> 20) & 3u);
         const u32x4* a0 = wide ? W : deep ? reinterpret_cast<const u32x4*>(t.rec) + node : ((act && !skip) ? T + slot : F);
-        const uint8_t* a1 = (deep && !wide && (int64_t)d <= i - stream_start) ? text + (i - d) : dummy;
+        const uint8_t* a1 = (deep && !wide && (int64_t)d <= i - stream_start) ? text + ((i - d) & ~(int64_t)7) : dummy;
         r.L0 = *a0;
-        r.tc = *a1;
+        r.tw = *reinterpret_cast<const u32x2*>(a1);
         r.n = take;
         qh += take;
         qn -= take;
@@ -633,8 +634,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         // (the compiler otherwise speculates it up to the loads and waits).
         // (Fenced copies: the round's own registers are never redefined.)
         u32x4 L0 = r.L0;
-        uint32_t tc = r.tc, fk = r.fk, fp = r.fp;
-        asm volatile("" : "+v"(L0), "+v"(tc), "+v"(fk), "+v"(fp)::"memory");
+        u32x2 tw = r.tw;
+        uint32_t fk = r.fk, fp = r.fp;
+        asm volatile("" : "+v"(L0), "+v"(tw), "+v"(fk), "+v"(fp)::"memory");
         bool again = false, wstep = false;
         uint32_t nk = 0, np = 0;
         if ((uint32_t)lane < r.n && !r.skip) {
@@ -690,10 +692,20 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 v = R.y;
                 if ((int64_t)d < avail) {
                     const uint32_t kind = rec_kind(R);
-                    if (kind == RT_REC_CHAIN_K) {  // one step of the run (the tail takes several)
-                        if (tc == (R.w >> 24)) {
-                            node = R.x & 0xFFFFFFu;
-                            ++d;
+                    const uint32_t ro = (uint32_t)(i - d) & 7u;  // text[i-d] in the 8-byte window
+                    const uint32_t tc = (((ro & 4) ? tw.y : tw.x) >> (8 * (ro & 3))) & 0xFFu;
+                    if (kind == RT_REC_CHAIN_K) {
+                        // the run's bytes against text[i-d], text[i-d-1], ...
+                        // as far as the window, the run and the stream allow
+                        const uint64_t win = ((uint64_t)tw.y << 32 | tw.x) << (8 * (7 - ro));
+                        const uint64_t dif = win ^ ((uint64_t)R.w << 32 | R.z);
+                        const uint32_t meq = dif ? (uint32_t)__builtin_clzll(dif) >> 3 : 8u;
+                        const uint32_t clen = (R.x >> 24) & 63u;
+                        const uint32_t cav = (uint32_t)(avail - d);
+                        const uint32_t cm = min(meq, min(min(clen, ro + 1u), cav));
+                        if (cm >= 1u && (cm == clen || (cm == ro + 1u && cm < cav))) {
+                            node = (R.x & 0xFFFFFFu) + cm - 1u;
+                            d += cm;
                             again = true;
                         }
                     } else if (kind == RT_REC_KIDS_K) {
