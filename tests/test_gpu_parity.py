@@ -560,6 +560,42 @@ def test_full_size_binary_and_deep_streams_kernels_agree(stream):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.slow
+def test_large_automaton_uses_the_uncoded_dfa():
+    """A dictionary of more than 2^20 automaton states: the DFA image keeps
+    plain transitions (the coded word has 20 state bits, pm_flatten.h) and
+    runs dfa_scan_kernel; it must still equal the RT kernel and a brute
+    force on a stream that contains the patterns."""
+    import torch
+    rng = np.random.default_rng(21)
+    pats = [bytes(rng.integers(0x20, 0x7F, size=int(L), dtype=np.uint8)) for L in rng.integers(20, 40, size=40000)]
+    d = pm.Dictionary(patterns=pats)
+    ac, rt = pm.HipMatcher("ac"), pm.HipMatcher("rt")
+    for m in (ac, rt):
+        m.add_dictionary(d)
+        m.compile()
+    n = 1 << 20
+    text = np.frombuffer(b"".join(pats[int(k)] for k in rng.integers(0, len(pats), size=n // 20)), np.uint8)[:n]
+    a = ac.read_block_codes(text)
+    b = rt.read_block_codes(text)
+    assert np.array_equal(a, b)
+    codes = {}
+    for i in range(d.n):
+        f, l, by = d.pattern(i)
+        codes[by] = (f << 24) | l
+    tb = text[:20000].tobytes()
+    for i in range(len(tb)):
+        exp = 0
+        for k in range(min(40, i + 1), 0, -1):
+            c = codes.get(tb[i + 1 - k:i + 1])
+            if c is not None:
+                exp = c
+                break
+        assert a[i] == exp, i
+    ac.free()
+    rt.free()
+
+
 def test_lines_stream_generator_and_kernels():
     """The lines stream (random dictionary patterns back to back): device
     bytes == host bytes; on 64 MiB of it RT, AC and auto agree at every
