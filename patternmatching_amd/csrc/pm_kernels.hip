@@ -807,6 +807,15 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             for (int j = 0; j < 16; ++j) fw[j] = s_f[rt_fhash(RT_RAW(j)) >> 20];  // the multiply reads 24 bits
 #pragma unroll
             for (int j = 0; j < 16; ++j) cm |= ((res[j] >> 15) & rt_fhit(fw[j], rt_fhash(RT_RAW(j)))) << j;
+            // count-only: a nonzero depth-2 answer stays nonzero however deep
+            // the walk goes (the answer is the deepest pattern on it), so only
+            // positions whose placeholder is 0 can change the count
+            if (OUTW == 0) {
+                uint32_t zm = 0;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) zm |= (uint32_t)((res[j] & 0x7FFFu) == 0u) << j;
+                cm &= zm;
+            }
         }
 #undef RT_KEY
 #undef RT_RAW
