@@ -527,7 +527,12 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     //         0.733 / 0.832 / 8.63 (V9 on the same box 0.763 / 0.879 / 7.95)
     // So the product: u32 = V8, count = V10, u16 = issue-time stage 2.
     constexpr bool kPushS2 = V == 8 || V == 9 || (V == 0 && OUTW == 4);
-    constexpr bool kRounds = !(V == 9 || V == 10 || (V == 0 && OUTW == 0));
+    constexpr bool kRounds = !(V == 9 || V == 10 || ((V == 0 || V == 12) && OUTW == 0));
+    // the stage-1 LDS filter; count-only without it (V = 0) queues every
+    // zero-placeholder position under a depth-2 node with children (2.3%
+    // of random-ASCII positions on snort) for the tail's batched stage 2
+    // (V = 12 keeps it, timing)
+    constexpr bool kStage1 = !(V == 0 && OUTW == 0);
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -801,12 +806,17 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         uint32_t cm = 0;  // bit j: position j goes past depth 2
 #pragma unroll
         for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
-        if (kFilter) {
+        if (kFilter && kStage1) {
             uint32_t fw[16];
 #pragma unroll
             for (int j = 0; j < 16; ++j) fw[j] = s_f[rt_fhash(RT_RAW(j)) >> 20];  // the multiply reads 24 bits
 #pragma unroll
             for (int j = 0; j < 16; ++j) cm |= ((res[j] >> 15) & rt_fhit(fw[j], rt_fhash(RT_RAW(j)))) << j;
+        } else if (kFilter) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) cm |= (res[j] >> 15) << j;
+        }
+        if (kFilter) {
             // count-only: a nonzero depth-2 answer stays nonzero however deep
             // the walk goes (the answer is the deepest pattern on it), so only
             // positions whose placeholder is 0 can change the count
@@ -1349,6 +1359,7 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 8: RT_LAUNCH(8); break;
         case 9: RT_LAUNCH(9); break;
         case 10: RT_LAUNCH(10); break;
+        case 12: RT_LAUNCH(12); break;
         default: RT_LAUNCH(0);
     }
 #undef RT_LAUNCH
