@@ -919,7 +919,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                         qkey[sl] = q32;
                         qpos[sl] = p;
                     } else {
-                        const uint32_t ph = (s_t[q32 >> 16] & 0x7FFFu) != 0u;
+                        // (count-only queues zero placeholders only)
+                        const uint32_t ph = OUTW == 0 ? 0u : (uint32_t)((s_t[q32 >> 16] & 0x7FFFu) != 0u);
                         reinterpret_cast<u32x2*>(sp)[sn + rank - room] = u32x2{q32, p | (ph << 31)};
                     }
                     ++rank;
