@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--mode", default="dense", choices=list(WIDTH),
                    help="dense: u32 id per position; dense16: u16 id per position; count: match count only")
     p.add_argument("--kernel", default="rt", choices=["rt", "ac", "auto"],
-                   help="rt: reverse-trie kernel; ac: the AC dense DFA; auto: both, picked per launch")
+                   help="rt: reverse-trie kernel; ac: the AC-DFA (dense rows or rows + records, timed); "
+                        "auto: RT or the AC-DFA, picked per launch")
     p.add_argument("--stream", default="ascii", choices=["ascii", "bytes", "ship", "lines"],
                    help="ascii / bytes: seeded synthetic (DESIGN.md §5); ship: the reference's shipped "
                         "dictionaries_generated.stream tiled to --bytes (adversarial: deep matches)")
@@ -195,7 +196,11 @@ def main():
     def step():
         m.scan_device(text.data_ptr(), 0, pos0, n, out_ptr, count.data_ptr(), stream.cuda_stream, out_width=width or 4)
 
-    for _ in range(args.warmup):
+    # ac / auto pick their kernel by timing it (an RT launch, then two launches
+    # of each DFA form): let that finish before the W warmups so the timed
+    # steps run the held choice (pm_plugin.hip AUTO_HOLD)
+    pick_launches = {"rt": 0, "ac": 5, "auto": 6}[args.kernel]
+    for _ in range(pick_launches + args.warmup):
         step()
     torch.cuda.synchronize()
     if use_dist:
@@ -241,7 +246,7 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             c = [int(v) for v in sc.tolist()]
-            extra["accuracy"] = {"reliable": "AC dense DFA (HIP)", "positions": n, "success": c[0],
+            extra["accuracy"] = {"reliable": "AC-DFA (HIP)", "positions": n, "success": c[0],
                                  "false_pos_rate": c[3] / n, "false_neg_rate": c[2] / n, "partial_rate": c[1] / n,
                                  "score_ms": round(e0.elapsed_time(e1), 4)}
             del ref
@@ -285,6 +290,7 @@ def main():
                              "(pm_hip_debug_scan_variant); kernel_over_floor = kernel_ms / floor kernel_ms"}
 
     if rank == 0:
+        last_kernel = "RT" if m.kernel_last == 1 else {1: "AC dense rows", 2: "AC rows + records"}.get(m.dfa_form_last, "?")
         total_bytes = world * args.bytes * args.steps  # every rank scans --bytes positions
         value = total_bytes / elapsed / 1e9
         alg_per_pos = 1 + width  # 1 B read + the id written per position
@@ -317,10 +323,11 @@ def main():
                 "dict": args.dict,
                 "stream_bytes_per_gpu": n,
                 "mode": args.mode,
-                "kernel": ("auto: RT, or the AC-DFA when a deep RT launch (spill > 10%%) is slower than a timed AC trial "
-                           "(last launch: %s)"
-                           % {1: "RT", 2: "AC"}.get(m.kernel_last, "?") if args.kernel == "auto" else
-                           {"rt": "reverse-suffix-trie walk", "ac": "Aho-Corasick dense DFA"}[args.kernel]),
+                "kernel": ("auto: RT, or after a deep RT launch (spill > 10%%) the fastest of RT and timed trials of "
+                           "both AC-DFA forms (last launch: %s)" % last_kernel if args.kernel == "auto" else
+                           "Aho-Corasick DFA, the faster of its two forms by timed trials (last launch: %s)" % last_kernel
+                           if args.kernel == "ac" else "reverse-suffix-trie walk"),
+                "pick_launches": pick_launches,
                 "parallelism": (f"independent stream shards x{world}" if args.layout == "shards" else
                                 f"one {world * args.bytes} B stream split x{world} (max_len-1 B context per shard)"),
                 "layout": args.layout,

@@ -140,6 +140,9 @@ int pm_hip_kernel_kind(void* obj);
 /* The kernel of the object's last launch: 1 = reverse trie, 2 = AC DFA
  * (0 before any). */
 int pm_hip_kernel_last(void* obj);
+/* DFA form of the last launch: 1 = dense rows, 2 = rows + 16-B records
+ * (pm_flatten.h), 0 = the RT kernel ran. */
+int pm_hip_dfa_form_last(void* obj);
 /* Seconds of device time of the scan kernels issued through read_block
  * since the last reset (hipEvent based). */
 double pm_hip_device_seconds(void* obj);
@@ -166,6 +169,12 @@ void pm_hip_debug_dfa_min_seg(int min_seg);
 /* Timing sweeps only: segments per lane of the output-coded AC-DFA kernel
  * (1 or 2; 0 = default). */
 void pm_hip_debug_dfa_chains(int chains);
+/* Timing sweeps only: the AC-DFA form of output-coded automata, 1 = sparse
+ * (rows + 16-B default-transition records, pm_flatten.h), 0 = dense rows,
+ * -1 = default. */
+void pm_hip_debug_dfa_sparse(int sparse);
+/* Timing sweeps only: positions per block of the sparse AC-DFA kernel (16 or 32; 0 = default). */
+void pm_hip_debug_dfa_block(int blk);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */
@@ -175,7 +184,10 @@ void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int
 void* pm_flat_build_cached(const char* const* pats, const uint32_t* lens, size_t n, int kind, const char* cache_dir);
 int pm_flat_cache_hit(void* handle);
 int pm_flat_fits(void* handle);
-/* name: "t12" "filt" "t3h" "rec" "next" "out" "index_of_gid" "parent" "depth"; returns element count */
+/* States with full rows in the sparse DFA form (0 when it has none). */
+uint32_t pm_flat_dfa_sparse_rows(void* handle);
+/* name: "t12" "filt" "t3h" "rec" "next" "out" "sblock" "sout" "index_of_gid" "parent" "depth";
+ * returns element count */
 size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* elem_size);
 void pm_flat_free(void* handle);
 

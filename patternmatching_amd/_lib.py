@@ -102,6 +102,7 @@ SIGNATURES = {
     "pm_hip_gid_index": (ctypes.c_uint32, [c_vp, ctypes.c_uint32]),
     "pm_hip_kernel_kind": (ctypes.c_int, [c_vp]),
     "pm_hip_kernel_last": (ctypes.c_int, [c_vp]),
+    "pm_hip_dfa_form_last": (ctypes.c_int, [c_vp]),
     "pm_hip_device_seconds": (ctypes.c_double, [c_vp]),
     "pm_hip_table_bytes": (ctypes.c_size_t, [c_vp]),
     "pm_hip_last_error": (ctypes.c_char_p, []),
@@ -112,12 +113,15 @@ SIGNATURES = {
     "pm_hip_debug_dfa_shape": (None, [ctypes.c_int]),
     "pm_hip_debug_dfa_min_seg": (None, [ctypes.c_int]),
     "pm_hip_debug_dfa_chains": (None, [ctypes.c_int]),
+    "pm_hip_debug_dfa_sparse": (None, [ctypes.c_int]),
+    "pm_hip_debug_dfa_block": (None, [ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
     "pm_flat_build_cached": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.c_char_p]),
     "pm_flat_cache_hit": (ctypes.c_int, [c_vp]),
     "pm_flat_fits": (ctypes.c_int, [c_vp]),
+    "pm_flat_dfa_sparse_rows": (ctypes.c_uint32, [c_vp]),
     "pm_flat_array": (ctypes.c_size_t, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
                                         ctypes.POINTER(ctypes.c_size_t)]),
     "pm_flat_free": (None, [c_vp]),

@@ -355,6 +355,63 @@ PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap&
     return r;
 }
 
+// The sparse form (pm_flatten.h).  order: states by depth, so a state's
+// failure (shallower) is decided before it.  The fallback of v is fail[v]
+// when that keeps a row, else fail[v]'s own fallback; then delta(v, c) =
+// next[v][c] = next[fallback][c] except at the bytes where the two rows
+// differ, and v becomes a record when those are at most PM_SDFA_K.
+static void build_sparse(DfaImage& im, const std::vector<uint32_t>& fail, const std::vector<uint32_t>& order) {
+    const uint32_t S = im.states;
+    std::vector<uint32_t> fb(S, UINT32_MAX);  // fallback (old numbering) of a record; UINT32_MAX = row
+    std::vector<uint32_t> slots(S, 0);         // record x word (bytes still in the old numbering's row)
+    for (uint32_t v : order) {
+        if (v == 0) continue;
+        const uint32_t f = fb[fail[v]] == UINT32_MAX ? fail[v] : fb[fail[v]];
+        const uint32_t* a = &im.next[(size_t)v * 256];
+        const uint32_t* b = &im.next[(size_t)f * 256];
+        uint32_t nd = 0, x = 0;
+        for (uint32_t c = 0; c < 256 && nd <= PM_SDFA_K; ++c)
+            if (a[c] != b[c]) {
+                if (nd < PM_SDFA_K) x |= (c | 0x100u) << (16 * nd);
+                ++nd;
+            }
+        if (nd <= PM_SDFA_K) {
+            fb[v] = f;
+            slots[v] = x;
+        }
+    }
+    // new ids in the trie's own order (depth-first below PM_DFA_DFS_DEPTH):
+    // the records of a unary run of states are then consecutive 16-B
+    // entries, eight to a 128-B line, so a walk along a pattern re-reads the
+    // line it just fetched instead of one new line per byte
+    std::vector<uint32_t> nid(S);
+    uint32_t F = 0;
+    for (uint32_t v = 0; v < S; ++v)
+        if (fb[v] == UINT32_MAX) nid[v] = F++;
+    uint32_t r = F;
+    for (uint32_t v = 0; v < S; ++v)
+        if (fb[v] != UINT32_MAX) nid[v] = r++;
+    auto remap = [&](uint32_t w) { return nid[w & PM_DFA_STATE_MASK] | (w & ~PM_DFA_STATE_MASK); };
+    im.sF = F;
+    im.sblock.assign((size_t)F * 256 + (size_t)(S - F) * PM_SDFA_REC_WORDS, 0);
+    im.sout.assign(S, 0);
+    for (uint32_t v = 0; v < S; ++v) {
+        im.sout[nid[v]] = im.out[v];
+        const uint32_t* a = &im.next[(size_t)v * 256];
+        if (fb[v] == UINT32_MAX) {
+            uint32_t* row = &im.sblock[(size_t)nid[v] * 256];
+            for (uint32_t c = 0; c < 256; ++c) row[c] = remap(a[c]);
+            continue;
+        }
+        uint32_t* R = &im.sblock[(size_t)F * 256 + (size_t)(nid[v] - F) * PM_SDFA_REC_WORDS];
+        const uint32_t x = slots[v];
+        R[0] = x;
+        R[1] = (x & 0x100u) ? remap(a[x & 0xFFu]) : 0u;
+        R[2] = (x & 0x1000000u) ? remap(a[(x >> 16) & 0xFFu]) : 0u;
+        R[3] = nid[fb[v]];
+    }
+}
+
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
     DfaImage im;
     BfsTrie t = build_trie(pats, g, /*reversed=*/false, PM_DFA_DFS_DEPTH);
@@ -387,8 +444,10 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
         im.out[v] = v == 0 ? 0 : (t.gid[v] ? t.gid[v] : im.out[fail[v]]);
     }
     // output-coded transitions (pm_flatten.h): target | code << 20
-    if (pm_dfa_coded(S))
+    if (pm_dfa_coded(S)) {
         for (uint32_t& x : im.next) x |= std::min(im.out[x], PM_DFA_ESC) << 20;
+        build_sparse(im, fail, by_depth);
+    }
     return im;
 }
 
@@ -397,7 +456,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 9;                     // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 10;                    // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);
@@ -429,11 +488,12 @@ bool save(const std::string& path, uint64_t key, int kind, const PmImages& im) {
     if (!f) return false;
     const uint32_t hdr[2] = {IMG_VERSION, (uint32_t)kind};
     const std::vector<uint32_t> scal = {im.rt.fits ? 1u : 0u, im.rt.t3h_bits, im.rt.n2int, im.rt.nrec, im.rt.nodes,
-                                        im.rt.d3, im.dfa.states, im.rt.nwide};
+                                        im.rt.d3, im.dfa.states, im.rt.nwide, im.dfa.sF};
     bool ok = std::fwrite(&IMG_MAGIC, 8, 1, f) == 1 && std::fwrite(&key, 8, 1, f) == 1 && std::fwrite(hdr, 4, 2, f) == 2 &&
               put(f, 1, scal) && put(f, 2, im.rt.t12) && put(f, 3, im.rt.filt) && put(f, 4, im.rt.t3h) &&
               put(f, 5, im.rt.rec) && put(f, 6, im.dfa.next) && put(f, 7, im.dfa.out) && put(f, 8, im.par.parent) &&
-              put(f, 9, im.par.depth) && put(f, 10, im.rt.wide);
+              put(f, 9, im.par.depth) && put(f, 10, im.rt.wide) && put(f, 11, im.dfa.sblock) &&
+              put(f, 12, im.dfa.sout);
     ok = (std::fclose(f) == 0) && ok;
     if (ok) ok = std::rename(tmp.c_str(), path.c_str()) == 0;
     if (!ok) std::remove(tmp.c_str());
@@ -448,9 +508,10 @@ bool load(const std::string& path, uint64_t key, int kind, PmImages& im) {
     std::vector<uint32_t> scal;
     bool ok = std::fread(&magic, 8, 1, f) == 1 && std::fread(&k, 8, 1, f) == 1 && std::fread(hdr, 4, 2, f) == 2 &&
               magic == IMG_MAGIC && k == key && hdr[0] == IMG_VERSION && hdr[1] == (uint32_t)kind &&
-              get(f, 1, scal) && scal.size() == 8 && get(f, 2, im.rt.t12) && get(f, 3, im.rt.filt) &&
+              get(f, 1, scal) && scal.size() == 9 && get(f, 2, im.rt.t12) && get(f, 3, im.rt.filt) &&
               get(f, 4, im.rt.t3h) && get(f, 5, im.rt.rec) && get(f, 6, im.dfa.next) && get(f, 7, im.dfa.out) &&
-              get(f, 8, im.par.parent) && get(f, 9, im.par.depth) && get(f, 10, im.rt.wide);
+              get(f, 8, im.par.parent) && get(f, 9, im.par.depth) && get(f, 10, im.rt.wide) &&
+              get(f, 11, im.dfa.sblock) && get(f, 12, im.dfa.sout);
     char extra;
     ok = ok && std::fread(&extra, 1, 1, f) == 0;  // nothing after the last section
     std::fclose(f);
@@ -463,6 +524,7 @@ bool load(const std::string& path, uint64_t key, int kind, PmImages& im) {
     im.rt.d3 = scal[5];
     im.dfa.states = scal[6];
     im.rt.nwide = scal[7];
+    im.dfa.sF = scal[8];
     // structural checks: the kernels index these tables without bounds
     if (kind == 1 && im.rt.fits &&
         (im.rt.t12.size() != RT_T1_BASE + 256 || im.rt.filt.size() != RT_FILTER_WORDS + RT_F2_WORDS ||
@@ -471,6 +533,10 @@ bool load(const std::string& path, uint64_t key, int kind, PmImages& im) {
          im.rt.wide.size() != (size_t)im.rt.nwide * RT_WIDE_WORDS))
         return false;
     if (kind == 2 && (im.dfa.next.size() != (size_t)im.dfa.states * 256 || im.dfa.out.size() != im.dfa.states))
+        return false;
+    if (kind == 2 && pm_dfa_coded(im.dfa.states) &&
+        (im.dfa.sF < 1 || im.dfa.sF > im.dfa.states || im.dfa.sout.size() != im.dfa.states ||
+         im.dfa.sblock.size() != (size_t)im.dfa.sF * 256 + (size_t)(im.dfa.states - im.dfa.sF) * PM_SDFA_REC_WORDS))
         return false;
     return true;
 }
@@ -496,6 +562,24 @@ bool values_ok(const PmImages& im, int kind, size_t ngid) {
         for (uint32_t x : im.dfa.next) {
             const uint32_t t = coded ? x & PM_DFA_STATE_MASK : x;
             if (t >= im.dfa.states || (coded && (x >> 20) != std::min(im.dfa.out[t], PM_DFA_ESC))) return false;
+        }
+        if (!coded) return true;
+        // sparse form: coded words consistent with sout, fallbacks are rows
+        const DfaImage& d = im.dfa;
+        auto word_ok = [&](uint32_t x) {
+            const uint32_t t = x & PM_DFA_STATE_MASK;
+            return t < d.states && (x >> 20) == std::min(d.sout[t], PM_DFA_ESC);
+        };
+        for (uint32_t x : d.sout)
+            if (x > P) return false;
+        const size_t nrow = (size_t)d.sF * 256;
+        for (size_t e = 0; e < nrow; ++e)
+            if (!word_ok(d.sblock[e])) return false;
+        for (size_t e = nrow; e < d.sblock.size(); e += PM_SDFA_REC_WORDS) {
+            const uint32_t* R = &d.sblock[e];
+            if ((R[0] & ~0x01FF01FFu) || R[3] >= d.sF) return false;
+            if ((R[0] & 0x100u) && !word_ok(R[1])) return false;
+            if ((R[0] & 0x1000000u) && !word_ok(R[2])) return false;
         }
         return true;
     }
@@ -565,7 +649,8 @@ uint64_t pm_image_key(const std::vector<std::string>& pats, int kind) {
     // few keys): a change to either gives new keys, not a stale hit
     uint32_t lay[] = {RT_T1_BASE, RT_CONT16, RT_CONT32, (uint32_t)RT_REC_WORDS, RT_FILTER_WORDS, RT_F3_WORDS,
                       RT_F4_WORDS, RT_T3H_INLINE, RT_T3H_VALID, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                      RT_REC_INLINE, (uint32_t)RT_WIDE_WORDS, (uint32_t)PM_DFA_DFS_DEPTH, RT_CHAIN_MAX};
+                      RT_REC_INLINE, (uint32_t)RT_WIDE_WORDS, (uint32_t)PM_DFA_DFS_DEPTH, RT_CHAIN_MAX,
+                      PM_SDFA_K, PM_SDFA_REC_WORDS};
     const uint32_t probe[2] = {0x00A1B2C3u, 0x00FFFFFFu};
     for (int q = 0; q < 2; ++q) {
         const uint32_t k = probe[q];

@@ -61,7 +61,8 @@
 //  DfaImage the Aho-Corasick automaton of Core/src/mpac.c (goto + BFS
 //           failure links + suffix/output links, :147-210) flattened into a
 //           dense DFA: next[s*256 + c] and out[s] (gid of the longest pattern
-//           that is a suffix of state s, 0 if none), states BFS-numbered;
+//           that is a suffix of state s, 0 if none), states numbered
+//           breadth-first to PM_DFA_DFS_DEPTH, depth-first below;
 //           below 2^20 states next also carries the target's output code
 //           (pm_dfa_coded, below).
 //
@@ -103,11 +104,33 @@ constexpr uint32_t PM_DFA_STATE_MASK = 0xFFFFFu;
 constexpr uint32_t PM_DFA_ESC = 4095u;
 inline bool pm_dfa_coded(uint32_t states) { return states <= PM_DFA_STATE_MASK; }
 
+// Sparse (default-transition) form of the same automaton, built only when
+// it is output-coded.  A state whose dense row differs from the row of its
+// fallback -- the first state with a full row on its failure chain -- in at
+// most PM_SDFA_K bytes keeps a 16-B record instead of a 1 KiB row:
+//   x = (c0 | 0x100) | (c1 | 0x100) << 16 (a missing slot is 0), y / z =
+//   the coded transitions on c0 / c1, w = the fallback's state (< F).
+// States are renumbered: full rows [0, F) (the root is 0), records [F, S),
+// both in the trie's order (depth-first below PM_DFA_DFS_DEPTH, so a unary
+// run of records is consecutive), and every coded word carries the new
+// numbering.  The
+// device keeps one block `rows (F * 1 KiB) | records ((S - F) * 16 B)`, so a
+// step is one 16-B load at offset s * 1024 + (c & ~3) * 4 (row) or F * 1024
+// + (s - F) * 16 (record), plus, at a record whose slots miss the byte, one
+// 4-B load of row w.  out is indexed by the new numbering.
+constexpr uint32_t PM_SDFA_K = 2;
+constexpr uint32_t PM_SDFA_REC_WORDS = 4;
+
 struct DfaImage {
     std::vector<uint32_t> next;  // states * 256 (output-coded when pm_dfa_coded(states))
     std::vector<uint32_t> out;   // states
     uint32_t states = 0;
+    // sparse form (pm_dfa_coded(states) only; empty otherwise)
+    std::vector<uint32_t> sblock;  // F * 256 row words, then (states - F) * 4 record words
+    std::vector<uint32_t> sout;    // states, new numbering
+    uint32_t sF = 0;
     size_t bytes() const { return next.size() * 4 + out.size() * 4; }
+    size_t sparse_bytes() const { return sblock.size() * 4 + sout.size() * 4; }
 };
 
 // Pattern suffix relation in gid space (the reference's patterns tree,
@@ -162,8 +185,9 @@ constexpr uint32_t RT_REC_INLINE = 8;  // children held inline in a record
 constexpr int RT_WIDE_WORDS = 16;
 // DFA state numbering: breadth-first to this depth, then children blocks in
 // depth-first order (build_trie), so a pattern's deep states are neighbours
+// (the dense rows do not care, 1 KiB each; the sparse form's 16-B records do)
 #ifndef PM_DFA_DFS_DEPTH
-#define PM_DFA_DFS_DEPTH 0xFFFFFFFFu
+#define PM_DFA_DFS_DEPTH 2u
 #endif
 inline uint32_t pm_rt_wide_word(uint32_t w) { return 4 * (w >> 1) + (w & 1); }  // bitmap word w in an entry
 constexpr uint32_t RT_FILTER_WORDS = 4096;  // stage 1: 16 KiB of LDS

@@ -29,6 +29,10 @@ struct DfaDev {
     const uint32_t* out;   // states
     int64_t warm;          // max pattern length - 1
     int coded;             // pm_dfa_coded(states)
+    const uint8_t* sbase;  // sparse form (coded only): rows | records block, pm_flatten.h
+    const uint32_t* sout;  // states, the sparse numbering
+    uint32_t sF;           // states with full rows
+    int form;              // 0 = the default (pm_dfa_set_sparse), 1 = dense rows, 2 = sparse
 };
 
 // Positions [pos0, pos0+n) of text; bytes back to stream_start are context.
@@ -47,6 +51,13 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 void pm_dfa_set_shape(int lanes_per_cu);
 void pm_dfa_set_chains(int chains);
 void pm_dfa_set_min_seg(int min_seg);
+// Timing sweeps: force the form of coded automata (1 = sparse, 0 = dense
+// rows) for launches whose DfaDev::form is 0; < 0 = no forced form (the
+// default form is then the sparse one).
+void pm_dfa_set_sparse(int sparse);
+bool pm_dfa_forced_form();
+void pm_dfa_set_block(int blk);  // sparse form, one chain: positions per block (16 or 32)
+bool pm_dfa_default_sparse();  // the form a launch with DfaDev::form 0 runs
 // counts[0..4] += success, partial, false_neg, false_pos, all_matches of algo
 // against real (n u32 gids each, 16-B aligned); parent/depth: PmParents.
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,

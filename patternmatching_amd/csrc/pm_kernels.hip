@@ -1160,6 +1160,151 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* _
     }
 }
 
+// Sparse (default-transition) DFA, pm_flatten.h: the same automaton with
+// rows only for the states whose row differs from their fallback's in more
+// than PM_SDFA_K bytes, 16-B records for the rest.  A step is one 16-B load
+// from one block (a row's aligned quad holding the byte, or the record) and,
+// at a record whose two slots miss the byte, one 4-B load of the fallback's
+// row.  On deep inputs the states a stream visits are mostly records: their
+// table is tens of MB instead of the dense rows' hundreds, so the loads stay
+// in L2 / the Infinity Cache instead of going to HBM.
+__device__ __forceinline__ uint32_t sdfa_off(uint32_t s, uint32_t c, uint32_t F) {
+    return s < F ? s * 1024u + (c & 0xFCu) * 4u : s * 16u + F * 1008u;  // F*1024 + (s-F)*16
+}
+
+template <int CH>
+__device__ __forceinline__ void sdfa_step(const uint8_t* __restrict__ base, uint32_t F, const uint32_t (&s)[CH],
+                                          const uint32_t (&c)[CH], uint32_t (&v)[CH]) {
+    uint4 q[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) q[k] = *reinterpret_cast<const uint4*>(base + sdfa_off(s[k], c[k], F));
+    bool miss[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const uint32_t key = c[k] | 0x100u;
+        const uint32_t rowv = (c[k] & 2u) ? ((c[k] & 1u) ? q[k].w : q[k].z) : ((c[k] & 1u) ? q[k].y : q[k].x);
+        const bool h0 = (q[k].x & 0x1FFu) == key, h1 = ((q[k].x >> 16) & 0x1FFu) == key;
+        const bool isrow = s[k] < F;
+        v[k] = isrow ? rowv : (h0 ? q[k].y : q[k].z);
+        miss[k] = !isrow && !h0 && !h1;
+    }
+#pragma unroll
+    for (int k = 0; k < CH; ++k)
+        if (miss[k]) v[k] = *reinterpret_cast<const uint32_t*>(base + q[k].w * 1024u + c[k] * 4u);
+}
+
+template <int OUTW, int CH, int BLK>
+__global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* __restrict__ text,
+                                                                 int64_t stream_start, int64_t pos0, int64_t n,
+                                                                 void* __restrict__ out,
+                                                                 unsigned long long* __restrict__ count,
+                                                                 const uint8_t* __restrict__ base, uint32_t F,
+                                                                 const uint32_t* __restrict__ outt, int64_t warm,
+                                                                 int64_t seg_len) {
+    const int64_t nseg = (n + seg_len - 1) / seg_len;
+    const int64_t lanes = (int64_t)gridDim.x * DFA_THREADS;
+    uint32_t cnt = 0;
+    for (int64_t sg0 = (int64_t)blockIdx.x * DFA_THREADS + threadIdx.x; sg0 < nseg; sg0 += CH * lanes) {
+        int64_t lo[CH], hi[CH], wlo[CH];
+        uint32_t s[CH];
+        int64_t wmax = 0;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int64_t sg = sg0 + k * lanes;
+            lo[k] = sg < nseg ? pos0 + sg * seg_len : pos0 + n;
+            hi[k] = sg < nseg ? (lo[k] + seg_len < pos0 + n ? lo[k] + seg_len : pos0 + n) : pos0 + n;
+            wlo[k] = lo[k] - warm;
+            if (wlo[k] < stream_start) wlo[k] = stream_start;
+            if (sg >= nseg) wlo[k] = lo[k];
+            s[k] = 0;
+            wmax = lo[k] - wlo[k] > wmax ? lo[k] - wlo[k] : wmax;
+        }
+        // warm-up: every chain from the root, right-aligned so they end together
+        for (int64_t j = wmax; j > 0; --j) {
+            uint32_t c[CH], v[CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) c[k] = lo[k] - j >= wlo[k] ? text[lo[k] - j] : 0u;
+            sdfa_step<CH>(base, F, s, c, v);
+#pragma unroll
+            for (int k = 0; k < CH; ++k) s[k] = lo[k] - j >= wlo[k] ? v[k] & DFA_STATE_MASK : s[k];
+        }
+        // blocks of BLK positions per chain: BLK / 16 16-B text loads, and
+        // the block's ids stored at once (BLK = 32: one whole 128-B line of
+        // u32 ids per lane, so the L2 never holds a half-written line)
+        constexpr int NW = BLK / 4;
+        const int64_t nblk = seg_len / BLK;
+        for (int64_t b = 0; b < nblk; ++b) {
+            bool act[CH];
+            uint32_t W[CH][NW];
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                act[k] = lo[k] + BLK * b + BLK <= hi[k];
+                any |= act[k];
+#pragma unroll
+                for (int q = 0; q < BLK / 16; ++q) {
+                    const uint4 w = act[k] ? *reinterpret_cast<const uint4*>(text + lo[k] + BLK * b + 16 * q)
+                                           : make_uint4(0, 0, 0, 0);
+                    W[k][4 * q] = w.x; W[k][4 * q + 1] = w.y; W[k][4 * q + 2] = w.z; W[k][4 * q + 3] = w.w;
+                }
+            }
+            if (!any) break;
+            uint32_t code[CH][BLK], st[CH][BLK];
+#pragma unroll
+            for (int j = 0; j < BLK; ++j) {
+                uint32_t c[CH], v[CH];
+#pragma unroll
+                for (int k = 0; k < CH; ++k) c[k] = (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                sdfa_step<CH>(base, F, s, c, v);
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    s[k] = act[k] ? v[k] & DFA_STATE_MASK : s[k];
+                    code[k][j] = v[k] >> 20;
+                    st[k][j] = s[k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                if (!act[k]) continue;
+                uint32_t r[BLK];
+#pragma unroll
+                for (int j = 0; j < BLK; ++j) r[j] = code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                const int64_t i = lo[k] + BLK * b;
+                if (OUTW == 4) {
+                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
+#pragma unroll
+                    for (int q = 0; q < BLK / 4; ++q) o[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+                }
+                if (OUTW == 2) {
+                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + (i - pos0));
+#pragma unroll
+                    for (int q = 0; q < BLK / 8; ++q)
+                        o[q] = make_uint4(r[8 * q] | r[8 * q + 1] << 16, r[8 * q + 2] | r[8 * q + 3] << 16,
+                                          r[8 * q + 4] | r[8 * q + 5] << 16, r[8 * q + 6] | r[8 * q + 7] << 16);
+                }
+#pragma unroll
+                for (int j = 0; j < BLK; ++j) cnt += r[j] != 0u;
+            }
+        }
+        // the segments' last (< BLK) positions, one chain at a time
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            for (int64_t i = lo[k] + BLK * ((hi[k] - lo[k]) / BLK); i < hi[k]; ++i) {
+                uint32_t s1[1] = {s[k]}, c1[1] = {text[i]}, v1[1];
+                sdfa_step<1>(base, F, s1, c1, v1);
+                s[k] = v1[0] & DFA_STATE_MASK;
+                const uint32_t v = outt[s[k]];
+                if (OUTW) put_id<OUTW>(out, i - pos0, v);
+                cnt += v != 0u;
+            }
+        }
+    }
+    if (count) {
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
+    }
+}
+
 // Accuracy of one id stream against a reference one (Core/src/measure.c:
 // 174-190 with is_pattern_suffix, PatternsTree.c:485-494), one position per
 // lane-element: equal -> success; algo on real's parent chain -> partial;
@@ -1396,8 +1541,20 @@ static int64_t g_dfa_min_seg = 0;  // pm_dfa_set_min_seg override (timing sweeps
 // two chains at 512 lanes per CU beat the uncoded kernel on random ASCII,
 // the tiled shipped stream and the lines stream; one chain lost on the
 // shipped stream)
-constexpr int DFA_CHAINS = 2;
-static int g_dfa_chains = DFA_CHAINS;
+// The sparse form (its step has a second, dependent load at a record miss)
+// measured best at one chain: lines stream 10.2 ms at 512 lanes x 1 against
+// 15.4 at x 2 (scripts/dfa_coded_sweep.py).
+constexpr int DFA_CHAINS = 2, SDFA_CHAINS = 1;
+// Positions per block of the sparse kernel at one chain (16 or 32;
+// pm_dfa_set_block): 32 stores one whole 128-B line of u32 ids per lane and
+// measured 6-15% faster on every stream (lines 10.23 -> 9.63 ms, shipped
+// 10.8 -> 9.7, ASCII 6.82 -> 6.15 at 512 lanes per CU; profiles/r02).
+constexpr int SDFA_BLK = 32;
+static int g_sdfa_blk = SDFA_BLK;
+static int g_dfa_chains = 0;  // 0: the form's default
+// dense rows or the sparse form for output-coded automata, when a launch
+// does not name one (-1: not forced; the plugin then times both forms)
+static int g_dfa_sparse = -1;
 
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s) {
@@ -1405,16 +1562,32 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (!out) outw = 0;
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
-    const int64_t ch = t.coded ? g_dfa_chains : 1;
+    const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
+    const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const int64_t lanes = (int64_t)num_cu * g_dfa_lanes_per_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
-    seg = (seg + 15) & ~(int64_t)15;
+    const int64_t align = sparse && ch == 1 ? g_sdfa_blk : 16;  // whole blocks per segment
+    seg = (seg + align - 1) / align * align;
     const int64_t nseg = (n + seg - 1) / seg;
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), b(DFA_THREADS);
+    if (sparse) {
+#define DS(W, C, B)                                                                                           \
+    hipLaunchKernelGGL((dfa_sparse_kernel<W, C, B>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.sbase, \
+                       t.sF, t.sout, t.warm, seg)
+        if (ch == 2) {
+            if (outw == 4) DS(4, 2, 16); else if (outw == 2) DS(2, 2, 16); else DS(0, 2, 16);
+        } else if (g_sdfa_blk == 32) {
+            if (outw == 4) DS(4, 1, 32); else if (outw == 2) DS(2, 1, 32); else DS(0, 1, 32);
+        } else {
+            if (outw == 4) DS(4, 1, 16); else if (outw == 2) DS(2, 1, 16); else DS(0, 1, 16);
+        }
+#undef DS
+        return hipGetLastError();
+    }
     if (t.coded) {
 #define DC(W, C) \
     hipLaunchKernelGGL((dfa_coded_kernel<W, C>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, t.out, t.warm, seg)
@@ -1437,7 +1610,11 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 
 void pm_dfa_set_shape(int lanes_per_cu) { g_dfa_lanes_per_cu = lanes_per_cu > 0 ? lanes_per_cu : DFA_LANES_PER_CU; }
 void pm_dfa_set_min_seg(int min_seg) { g_dfa_min_seg = min_seg >= 16 ? min_seg : 0; }
-void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : DFA_CHAINS; }
+void pm_dfa_set_sparse(int sparse) { g_dfa_sparse = sparse < 0 ? -1 : sparse != 0; }
+void pm_dfa_set_block(int blk) { g_sdfa_blk = blk == 16 || blk == 32 ? blk : SDFA_BLK; }
+bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
+bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
+void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }
 
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,
                           const uint32_t* depth, unsigned long long* counts, int num_cu, hipStream_t s) {

@@ -52,31 +52,38 @@ enum Kind { KIND_RT = 1, KIND_AC = 2, KIND_AUTO = 3 };
 // reports how many candidates it spilled (its queue overflowed: dense deep
 // matches -- DESIGN.md §4; a count-only launch, which queues nothing,
 // reports the positions its tail walked) and its time; when a launch
-// reported more than AUTO_SPILL_FRAC of its positions, the next AUTO_TRIAL
-// launches run the AC-DFA kernel, the last one timed (the first pays cold
-// caches), and whichever of the two took less per position
-// runs the next AUTO_HOLD launches; then RT measures again.  (Deep input is
-// where the DFA can win: on the tiled shipped stream it is 2.2x RT, on the
-// non-periodic lines stream RT is 1.4x the DFA.)  Counts and times come back
-// through pinned memory and events, waited for at the next launch (see
-// launch()).  reset() (a new stream) clears it.
+// reported more than AUTO_SPILL_FRAC of its positions, the next launches
+// try the AC-DFA kernel in each of its forms (dense rows, then rows +
+// records, pm_flatten.h), AUTO_TRIAL launches each, the last one timed (the
+// first pays cold caches), and whichever of the measured kernels took least
+// per position runs the next AUTO_HOLD launches; then RT measures again.
+// (Deep input is where the DFA can win: on the tiled shipped stream the
+// dense form is 2.2x RT, on the non-periodic lines stream the sparse form
+// is 1.4x RT and 2x the dense form.)  KIND_AC runs the same trials of its
+// two forms without the RT launch.  Counts and times come back through
+// pinned memory and events, waited for at the next launch (see launch()).
+// reset() (a new stream) clears it.
 constexpr double AUTO_SPILL_FRAC = 0.10;
 constexpr int AUTO_TRIAL = 2;
 constexpr int AUTO_HOLD = 64;
+enum Cand { CAND_RT = 0, CAND_DENSE = 1, CAND_SPARSE = 2, NCAND = 3 };
 
 struct AutoPick {
     unsigned long long* d_spill = nullptr;  // device counter of the last measured RT launch
     unsigned long long* h_spill = nullptr;  // pinned copy
     hipEvent_t ev = nullptr;                // the copy has landed
-    hipEvent_t rt0 = nullptr, rt1 = nullptr, ac0 = nullptr, ac1 = nullptr;  // timing of the measured launches
+    hipEvent_t t0[NCAND] = {}, t1[NCAND] = {};  // timing of each candidate's measured launch
     bool pending = false;     // a measured RT launch (spill count + time) in flight
-    bool ac_pending = false;  // a timed AC trial launch in flight
-    int trial = 0;            // AC trial launches left (the last one is timed)
-    int64_t n_last = 0, n_ac = 0;
-    double rt_ns = 0.0;       // the measured RT launch's ns per position
-    int dfa_left = 0;         // launches left on the chosen kernel (hold)
-    int chosen = 0;           // KIND_RT / KIND_AC during a hold
-    int last = 0;             // kernel of the last launch (KIND_RT / KIND_AC)
+    bool timing = false;      // the DFA trials are launched, their times in flight
+    int queue[2] = {0, 0};    // DFA forms to try, in order
+    int nq = 0, qi = 0;       // forms queued / started
+    int trial = 0;            // launches left of the form being tried (the last one timed)
+    int64_t n_of[NCAND] = {};
+    double ns[NCAND] = {};    // measured ns per position (0 = not measured this round)
+    int hold = 0;             // launches left on the chosen candidate
+    int chosen = CAND_RT;
+    int last = 0;             // KIND_RT / KIND_AC of the last launch
+    int last_form = 0;        // DFA form of the last launch: 1 dense rows, 2 sparse (0: RT)
 };
 
 // read_block pipeline blocks (positions): the upload, kernel and download of
@@ -146,13 +153,16 @@ struct PmHip {
     uint8_t* d_lines_pats = nullptr;
     uint32_t* d_lines_offs = nullptr;
     int last_kernel = 0;  // KIND_RT / KIND_AC of the last launch
+    int last_form = 0;    // its DFA form (1 dense rows, 2 sparse; 0 for RT)
 };
 
 void free_pick(AutoPick& a) {
     if (a.d_spill) (void)hipFree(a.d_spill);
     if (a.h_spill) (void)hipHostFree(a.h_spill);
-    for (hipEvent_t e : {a.ev, a.rt0, a.rt1, a.ac0, a.ac1})
-        if (e) (void)hipEventDestroy(e);
+    if (a.ev) (void)hipEventDestroy(a.ev);
+    for (int c = 0; c < NCAND; ++c)
+        for (hipEvent_t e : {a.t0[c], a.t1[c]})
+            if (e) (void)hipEventDestroy(e);
     a = AutoPick();
 }
 
@@ -257,73 +267,115 @@ void par_range(size_t n, size_t grain, const F& f) {
     for (auto& t : th) t.join();
 }
 
+hipError_t launch_cand(PmHip* o, AutoPick& ap, int c, const uint8_t* text, int64_t stream_start, int64_t pos0,
+                       int64_t n, void* out, int outw, unsigned long long* count, hipStream_t s, const RtDev& t) {
+    ap.last = c == CAND_RT ? KIND_RT : KIND_AC;
+    ap.last_form = c == CAND_RT ? 0 : c == CAND_SPARSE ? 2 : 1;
+    if (c == CAND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
+    DfaDev d = o->dfa;
+    d.form = c == CAND_SPARSE ? 2 : 1;
+    return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, d, o->num_cu, s);
+}
+
 hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                   unsigned long long* count, hipStream_t s, uint32_t* spill, int64_t spill_cap, AutoPick& ap) {
     RtDev t = o->rt;
     t.spill = spill;
     t.spill_cap = spill_cap;
     if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
-    if (o->kind == KIND_AC) return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
-    // KIND_AUTO (see AUTO_SPILL_FRAC): RT launches are measured (spill
-    // count and time); a deep one triggers one timed AC trial; the faster
-    // per position then runs AUTO_HOLD launches.  Results are read only once
-    // their events have completed, so no launch waits.
+    // one DFA form only (an uncoded automaton), or a form forced for timing
+    if (o->kind == KIND_AC && (!o->dfa.sbase || pm_dfa_forced_form())) {
+        ap.last = KIND_AC;
+        ap.last_form = o->dfa.sbase && pm_dfa_forced_form() && pm_dfa_default_sparse() ? 2 : 1;
+        return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+    }
+    // KIND_AUTO / KIND_AC (see AUTO_SPILL_FRAC): RT launches are measured
+    // (spill count and time); a deep one (or, for KIND_AC, the end of a
+    // hold) starts timed trials of the DFA forms; the fastest per position
+    // then runs AUTO_HOLD launches.  Results are read only once their events
+    // have completed, so no launch waits.
     if (!ap.ev) {
         PM_CHECK(hipMalloc(&ap.d_spill, sizeof(unsigned long long)));
         PM_CHECK(hipHostMalloc(&ap.h_spill, sizeof(unsigned long long), hipHostMallocDefault));
         PM_CHECK(hipEventCreateWithFlags(&ap.ev, hipEventDisableTiming));
-        for (hipEvent_t* e : {&ap.rt0, &ap.rt1, &ap.ac0, &ap.ac1}) PM_CHECK(hipEventCreate(e));
+        for (int c = 0; c < NCAND; ++c) {
+            PM_CHECK(hipEventCreate(&ap.t0[c]));
+            PM_CHECK(hipEventCreate(&ap.t1[c]));
+        }
     }
+    auto elapsed_ns = [&](int c) {
+        float ms = 0.f;
+        return hipEventElapsedTime(&ms, ap.t0[c], ap.t1[c]) == hipSuccess && ap.n_of[c] > 0
+                   ? ms * 1e6 / (double)ap.n_of[c]
+                   : 0.0;
+    };
+    auto start_trials = [&]() {
+        ap.nq = 0;
+        ap.queue[ap.nq++] = CAND_DENSE;
+        if (o->dfa.sbase) ap.queue[ap.nq++] = CAND_SPARSE;
+        ap.qi = 0;
+        ap.trial = 0;
+    };
     // measurements are waited for (not polled): a burst of device-side
     // launches would otherwise outrun them and never adapt; the wait is one
-    // host-side bubble per measurement, i.e. per AUTO_HOLD + AUTO_TRIAL + 1
+    // host-side bubble per measurement, i.e. per AUTO_HOLD + trials + 1
     // launches, and free in the read_block pipeline, which has synchronized
     // the slot already
     if (ap.pending && hipEventSynchronize(ap.ev) == hipSuccess) {
         ap.pending = false;
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, ap.rt0, ap.rt1) == hipSuccess) ap.rt_ns = ms * 1e6 / (double)ap.n_last;
-        if ((double)*ap.h_spill > AUTO_SPILL_FRAC * (double)ap.n_last) {
-            ap.trial = AUTO_TRIAL;
+        ap.ns[CAND_RT] = elapsed_ns(CAND_RT);
+        if ((double)*ap.h_spill > AUTO_SPILL_FRAC * (double)ap.n_of[CAND_RT]) {
+            start_trials();
         } else {  // shallow: RT holds
-            ap.chosen = KIND_RT;
-            ap.dfa_left = AUTO_HOLD;
+            ap.chosen = CAND_RT;
+            ap.hold = AUTO_HOLD;
         }
     }
-    if (ap.ac_pending && hipEventSynchronize(ap.ac1) == hipSuccess) {
-        ap.ac_pending = false;
-        float ms = 0.f;
-        const double ac_ns = hipEventElapsedTime(&ms, ap.ac0, ap.ac1) == hipSuccess ? ms * 1e6 / (double)ap.n_ac : 0.0;
-        ap.chosen = ac_ns > 0.0 && ac_ns < ap.rt_ns ? KIND_AC : KIND_RT;
-        ap.dfa_left = AUTO_HOLD;
+    if (ap.timing && hipEventSynchronize(ap.t1[ap.queue[ap.nq - 1]]) == hipSuccess) {
+        ap.timing = false;
+        int best = o->kind == KIND_AUTO ? CAND_RT : ap.queue[0];
+        double best_ns = o->kind == KIND_AUTO ? ap.ns[CAND_RT] : 0.0;
+        for (int k = 0; k < ap.nq; ++k) {
+            const int c = ap.queue[k];
+            ap.ns[c] = elapsed_ns(c);
+            if (ap.ns[c] > 0.0 && (best_ns <= 0.0 || ap.ns[c] < best_ns)) {
+                best = c;
+                best_ns = ap.ns[c];
+            }
+        }
+        ap.chosen = best;
+        ap.hold = AUTO_HOLD;
+        ap.nq = ap.qi = 0;
     }
-    hipError_t e = hipSuccess;
-    if (ap.dfa_left > 0) {  // hold the chosen kernel
-        --ap.dfa_left;
-        ap.last = ap.chosen;
-        if (ap.chosen == KIND_AC) return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
-        return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
+    if (ap.hold > 0) {  // hold the chosen kernel
+        --ap.hold;
+        return launch_cand(o, ap, ap.chosen, text, stream_start, pos0, n, out, outw, count, s, t);
     }
-    if (ap.trial > 0 && !ap.ac_pending) {  // AC trial launches; the last one is timed (the first pays cold caches)
-        ap.last = KIND_AC;
-        if (--ap.trial > 0) return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
-        e = hipEventRecord(ap.ac0, s);
-        if (e == hipSuccess) e = pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
-        if (e == hipSuccess) e = hipEventRecord(ap.ac1, s);
-        ap.ac_pending = e == hipSuccess;
-        ap.n_ac = n;
+    if (o->kind == KIND_AC && !ap.timing && ap.qi >= ap.nq) start_trials();
+    if (!ap.timing && ap.qi < ap.nq) {  // DFA trials: AUTO_TRIAL launches per form, the last one timed
+        const int c = ap.queue[ap.qi];
+        if (ap.trial == 0) ap.trial = AUTO_TRIAL;
+        if (--ap.trial > 0) return launch_cand(o, ap, c, text, stream_start, pos0, n, out, outw, count, s, t);
+        hipError_t e = hipEventRecord(ap.t0[c], s);
+        if (e == hipSuccess) e = launch_cand(o, ap, c, text, stream_start, pos0, n, out, outw, count, s, t);
+        if (e == hipSuccess) e = hipEventRecord(ap.t1[c], s);
+        ap.n_of[c] = n;
+        if (++ap.qi == ap.nq) ap.timing = e == hipSuccess;
         return e;
     }
+    if (ap.timing)  // (not reached: the wait above resolves it) keep the trials' last form
+        return launch_cand(o, ap, ap.queue[ap.nq - 1], text, stream_start, pos0, n, out, outw, count, s, t);
     ap.last = KIND_RT;
+    ap.last_form = 0;
     t.spill_total = ap.d_spill;
-    e = hipMemsetAsync(ap.d_spill, 0, sizeof(unsigned long long), s);
-    if (e == hipSuccess) e = hipEventRecord(ap.rt0, s);
+    hipError_t e = hipMemsetAsync(ap.d_spill, 0, sizeof(unsigned long long), s);
+    if (e == hipSuccess) e = hipEventRecord(ap.t0[CAND_RT], s);
     if (e == hipSuccess) e = pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
-    if (e == hipSuccess) e = hipEventRecord(ap.rt1, s);
+    if (e == hipSuccess) e = hipEventRecord(ap.t1[CAND_RT], s);
     if (e == hipSuccess) e = hipMemcpyAsync(ap.h_spill, ap.d_spill, sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipEventRecord(ap.ev, s);
     ap.pending = e == hipSuccess;
-    ap.n_last = n;
+    ap.n_of[CAND_RT] = n;
     return e;
 }
 
@@ -403,6 +455,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, narrow ? 2 : 4, nullptr,
                         q.stream, q.spill, q.spill_cap, q.pick));
         o->last_kernel = q.pick.last ? q.pick.last : o->kind;
+        o->last_form = q.pick.last_form;
         PM_CHECK(hipEventRecord(q.ev1, q.stream));
         if (narrow)
             PM_CHECK(hipMemcpyAsync(q.h_res, q.d_res, m * sizeof(uint16_t), hipMemcpyDeviceToHost, q.stream));
@@ -501,6 +554,11 @@ void pm_hip_compile(void* obj) {
         o->dfa.out = (const uint32_t*)dalloc_copy(o, im.dfa.out.data(), im.dfa.out.size() * 4);
         o->dfa.warm = o->max_len ? (int64_t)o->max_len - 1 : 0;
         o->dfa.coded = pm_dfa_coded(im.dfa.states) ? 1 : 0;
+        if (!im.dfa.sblock.empty()) {
+            o->dfa.sbase = (const uint8_t*)dalloc_copy(o, im.dfa.sblock.data(), im.dfa.sblock.size() * 4);
+            o->dfa.sout = (const uint32_t*)dalloc_copy(o, im.dfa.sout.data(), im.dfa.sout.size() * 4);
+            o->dfa.sF = im.dfa.sF;
+        }
     }
     o->d_parent = (const uint32_t*)dalloc_copy(o, im.par.parent.data(), im.par.parent.size() * 4);
     o->d_depth = (const uint32_t*)dalloc_copy(o, im.par.depth.data(), im.par.depth.size() * 4);
@@ -542,10 +600,10 @@ void pm_hip_reset(void* obj) {
     // belongs to the old stream: wait for it and drop it)
     auto forget = [](AutoPick& a) {
         if (a.pending) (void)hipEventSynchronize(a.ev);
-        if (a.ac_pending) (void)hipEventSynchronize(a.ac1);
-        a.pending = a.ac_pending = false;
-        a.trial = 0;
-        a.dfa_left = 0;
+        if (a.timing) (void)hipEventSynchronize(a.t1[a.queue[a.nq - 1]]);
+        a.pending = a.timing = false;
+        a.nq = a.qi = a.trial = 0;
+        a.hold = 0;
     };
     forget(o->pick);
     for (PipeSlot& q : o->slot) forget(q.pick);
@@ -604,6 +662,7 @@ static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
         e = launch(o, d_text, stream_start, pos0, n, d_out, outw, d_count, (hipStream_t)hip_stream, o->spill,
                    o->spill_cap, o->pick);
         o->last_kernel = o->pick.last ? o->pick.last : o->kind;
+        o->last_form = o->pick.last_form;
     }
     if (e != hipSuccess) {
         std::snprintf(g_err, sizeof(g_err), "launch: %s", hipGetErrorString(e));
@@ -685,6 +744,8 @@ int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int
 
 void pm_hip_debug_dfa_chains(int chains) { pm_dfa_set_chains(chains); }
 
+void pm_hip_debug_dfa_sparse(int sparse) { pm_dfa_set_sparse(sparse); }
+void pm_hip_debug_dfa_block(int blk) { pm_dfa_set_block(blk); }
 void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }
 void pm_hip_debug_dfa_min_seg(int min_seg) { pm_dfa_set_min_seg(min_seg); }
 
@@ -753,6 +814,7 @@ uint32_t pm_hip_gid_index(void* obj, uint32_t gid) {
 }
 int pm_hip_kernel_kind(void* obj) { return as(obj)->kind; }
 int pm_hip_kernel_last(void* obj) { return as(obj)->last_kernel; }
+int pm_hip_dfa_form_last(void* obj) { return as(obj)->last_form; }
 double pm_hip_device_seconds(void* obj) { return as(obj)->dev_seconds; }
 size_t pm_hip_table_bytes(void* obj) { return as(obj)->table_bytes; }
 
@@ -792,6 +854,8 @@ void* pm_flat_build(const char* const* pats, const uint32_t* lens, size_t n, int
 
 int pm_flat_cache_hit(void* handle) { return static_cast<PmFlatHandle*>(handle)->hit ? 1 : 0; }
 
+uint32_t pm_flat_dfa_sparse_rows(void* handle) { return static_cast<PmFlatHandle*>(handle)->dfa.sF; }
+
 int pm_flat_fits(void* handle) { return static_cast<PmFlatHandle*>(handle)->rt.fits ? 1 : 0; }
 
 size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* elem_size) {
@@ -809,6 +873,8 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
     if (s == "wide") return ret(h->rt.wide);
     if (s == "next") return ret(h->dfa.next);
     if (s == "out") return ret(h->dfa.out);
+    if (s == "sblock") return ret(h->dfa.sblock);
+    if (s == "sout") return ret(h->dfa.sout);
     if (s == "index_of_gid") return ret(h->g.index_of_gid);
     if (s == "parent") return ret(h->par.parent);
     if (s == "depth") return ret(h->par.depth);

@@ -224,6 +224,11 @@ class HipMatcher:
         return self.lib.pm_hip_kernel_kind(self.obj)
 
     @property
+    def dfa_form_last(self):
+        """1 = dense rows, 2 = rows + records (pm_flatten.h), 0 = RT ran."""
+        return self.lib.pm_hip_dfa_form_last(self.obj)
+
+    @property
     def kernel_last(self):
         """Kernel of the last launch: 1 = reverse trie, 2 = AC DFA."""
         return self.lib.pm_hip_kernel_last(self.obj)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Launch shape of the output-coded AC-DFA kernel: lanes per CU
+"""Form (dense rows / sparse rows + records) and launch shape of the
+output-coded AC-DFA kernel: lanes per CU
 (pm_hip_debug_dfa_shape) x segments per lane (pm_hip_debug_dfa_chains),
 snort, dense u32, on random ASCII, the shipped stream tiled and the lines
 stream; every shape's ids must equal the first one's.  Timing tool only."""
@@ -21,6 +22,9 @@ ap.add_argument("--bytes", type=int, default=1 << 30)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--lanes", default="256,512,1024")
 ap.add_argument("--streams", default="ascii,ship,lines")
+ap.add_argument("--forms", default="0,1", help="0 = dense rows, 1 = sparse rows + records (pm_hip_debug_dfa_sparse)")
+ap.add_argument("--chains", default="1,2")
+ap.add_argument("--blocks", default="16", help="sparse form, one chain: positions per block (16,32)")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 data = os.path.join(REPO, "tests", "golden", "data")
@@ -59,17 +63,23 @@ for stream in args.streams.split(","):
         ship = torch.from_numpy(np.fromfile(os.path.join(data, "dictionaries_generated.stream"), dtype=np.uint8))
         text.copy_(ship.cuda().repeat((n + 64) // ship.numel() + 1)[: n + 64])
     first = True
-    for lanes in [int(x) for x in args.lanes.split(",")]:
-        lib.pm_hip_debug_dfa_shape(lanes)
-        for ch in (1, 2):
-            lib.pm_hip_debug_dfa_chains(ch)
-            dst = ref if first else out
-            ms = timed(lambda: m.scan_device(text.data_ptr(), 0, 0, n, dst.data_ptr(), None, s.cuda_stream))
-            same = True if first else bool(torch.equal(out, ref))
-            first = False
-            key = f"{stream}/L{lanes}/ch{ch}"
-            res[key] = {"ms": round(ms, 4), "GBps": round(n / ms / 1e6, 1), "same": same}
-            print(stream, lanes, ch, res[key], flush=True)
+    for form in [int(x) for x in args.forms.split(",")]:
+        lib.pm_hip_debug_dfa_sparse(form)
+        for lanes in [int(x) for x in args.lanes.split(",")]:
+            lib.pm_hip_debug_dfa_shape(lanes)
+            for ch in [int(x) for x in args.chains.split(",")]:
+                lib.pm_hip_debug_dfa_chains(ch)
+                for blk in [int(x) for x in args.blocks.split(",")] if form and ch == 1 else [16]:
+                    lib.pm_hip_debug_dfa_block(blk)
+                    dst = ref if first else out
+                    ms = timed(lambda: m.scan_device(text.data_ptr(), 0, 0, n, dst.data_ptr(), None, s.cuda_stream))
+                    same = True if first else bool(torch.equal(out, ref))
+                    first = False
+                    key = f"{stream}/{'sparse' if form else 'dense'}/L{lanes}/ch{ch}/b{blk}"
+                    res[key] = {"ms": round(ms, 4), "GBps": round(n / ms / 1e6, 1), "same": same}
+                    print(key, res[key], flush=True)
 lib.pm_hip_debug_dfa_shape(0)
 lib.pm_hip_debug_dfa_chains(0)
+lib.pm_hip_debug_dfa_sparse(-1)
+lib.pm_hip_debug_dfa_block(0)
 print(json.dumps(res))

@@ -194,6 +194,39 @@ def dfa_scan(img, text):
     return res
 
 
+def sdfa_scan(img, text):
+    """dfa_sparse_kernel over the sparse form (pm_flatten.h): states below
+    F have full rows; a record {x = (c0|0x100) | (c1|0x100) << 16, y, z,
+    w = fallback} answers its two bytes and defers every other byte to row
+    w.  The codes are checked against sout at every step."""
+    F = int(img.lib.pm_flat_dfa_sparse_rows(img.h))
+    blk = img.array("sblock")
+    sout = img.array("sout")
+    assert F >= 1 and len(blk) == F * 256 + (len(sout) - F) * 4
+    rows = blk[: F * 256]
+    rec = blk[F * 256:].reshape(-1, 4)
+    s = 0
+    res = np.empty(len(text), np.uint32)
+    for j, c in enumerate(np.asarray(text, dtype=np.uint8).tolist()):
+        if s < F:
+            x = int(rows[s * 256 + c])
+        else:
+            R = rec[s - F]
+            key = c | 0x100
+            if int(R[0]) & 0x1FF == key:
+                x = int(R[1])
+            elif (int(R[0]) >> 16) & 0x1FF == key:
+                x = int(R[2])
+            else:
+                assert int(R[3]) < F
+                x = int(rows[int(R[3]) * 256 + c])
+        s = x & 0xFFFFF
+        code = x >> 20
+        assert code == min(int(sout[s]), 4095)
+        res[j] = code if code != 4095 else sout[s]
+    return res
+
+
 def gid_to_code(img, dictionary):
     idx = img.array("index_of_gid")
     codes = dictionary.codes()

@@ -625,6 +625,54 @@ def test_lines_stream_generator_and_kernels():
     assert np.array_equal(o.scan_codes(host), rt._codes[a[: 1 << 20].cpu().numpy().view(np.uint32)])
 
 
+@pytest.mark.parametrize("stream", ["ascii", "lines", "ship"])
+def test_sparse_dfa_equals_dense_dfa(stream):
+    """The AC kind's two forms of the output-coded automaton -- dense rows
+    (dfa_coded_kernel) and rows + default-transition records
+    (dfa_sparse_kernel, pm_flatten.h) -- give the same u32 / u16 ids and
+    counts at every position, at launch sizes from one segment with its
+    warm-up to 64 MiB, and equal the RT kernel."""
+    torch = _torch()
+    lib = pm.load()
+    rt, ac = matcher("snort", "rt"), matcher("snort", "ac")
+    n = 64 << 20
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    if stream == "ascii":
+        lib.pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 5, 0, s)
+    elif stream == "lines":
+        rt.gen_lines_device(dt.data_ptr(), n + 64, 9, s)
+    else:
+        dt.copy_(torch.from_numpy(np.tile(SHIP, (n + 64) // len(SHIP) + 1)[: n + 64]).cuda())
+    ref = torch.empty(n, dtype=torch.int32, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, ref.data_ptr(), None, s)
+    try:
+        for size, start in ((n, 0), (1000, 5000), (100 << 10, 12345), (3 << 20, 1 << 20)):
+            start &= ~15
+            got = {}
+            for sparse, blk in ((0, 16), (1, 16), (1, 32)):
+                lib.pm_hip_debug_dfa_sparse(sparse)
+                lib.pm_hip_debug_dfa_block(blk)
+                a = torch.zeros(size, dtype=torch.int32, device="cuda")
+                h = torch.zeros(size, dtype=torch.int16, device="cuda")
+                c = torch.zeros(3, dtype=torch.int64, device="cuda")
+                ac.scan_device(dt.data_ptr(), 0, start, size, a.data_ptr(), c[0:1].data_ptr(), s)
+                ac.scan_device(dt.data_ptr(), 0, start, size, h.data_ptr(), c[1:2].data_ptr(), s, out_width=2)
+                ac.scan_device(dt.data_ptr(), 0, start, size, 0, c[2:3].data_ptr(), s)
+                torch.cuda.synchronize()
+                got[(sparse, blk)] = (a, h, c)
+            a0, h0, c0 = got[(0, 16)]
+            for key in ((1, 16), (1, 32)):
+                a1, h1, c1 = got[key]
+                assert torch.equal(a0, a1) and torch.equal(h0, h1) and torch.equal(c0, c1), key
+            assert torch.equal(a1, ref[start:start + size])
+            assert int(c1[0].item()) == int(c1[2].item()) == int((a1 != 0).sum().item())
+            assert torch.equal(h1.to(torch.int32) & 0xFFFF, a1)
+    finally:
+        lib.pm_hip_debug_dfa_sparse(-1)
+        lib.pm_hip_debug_dfa_block(0)
+
+
 def test_adversarial_stream_large_rt_equals_ac():
     """A 32 MiB tiling of the shipped adversarial stream queues far more
     positions than the worklist holds, so the scan kernel's in-kernel
@@ -711,16 +759,50 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     want = torch.empty(n, dtype=torch.int32, device="cuda")
     ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
     m = matcher("et", "auto")
-    kernels = []
-    for _ in range(5):
+    kernels, forms = [], []
+    for _ in range(8):
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
         kernels.append(m.kernel_last)
+        forms.append(m.dfa_form_last)
         assert torch.equal(got, want)
-    # RT first (measured: it spills), then two AC trial launches (the second
-    # timed); the faster of the two per position holds after that
-    assert kernels[:3] == [pm.KIND_RT, pm.KIND_AC, pm.KIND_AC], kernels
+    # RT first (measured: it spills), then two trial launches of each DFA
+    # form (dense rows, then rows + records; the second of each timed); the
+    # fastest of the three per position holds after that
+    assert kernels[:5] == [pm.KIND_RT] + [pm.KIND_AC] * 4, kernels
+    assert forms[:5] == [0, 1, 1, 2, 2], forms
+    assert len(set(zip(kernels[5:], forms[5:]))) == 1, (kernels, forms)
+
+
+@pytest.mark.parametrize("stream", ["ship", "lines"])
+def test_ac_kind_times_both_dfa_forms(stream):
+    """The AC kind tries its two forms (two launches each, the second timed)
+    and holds the faster; every launch equals the RT kernel."""
+    import torch
+    n = 16 << 20
+    s = torch.cuda.current_stream()
+    rt, ac = matcher("snort", "rt"), matcher("snort", "ac")
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    if stream == "ship":
+        dt.copy_(torch.from_numpy(np.concatenate([_tiled_ship(n), np.zeros(64, np.uint8)])).cuda())
+    else:
+        rt.gen_lines_device(dt.data_ptr(), n + 64, 4, s.cuda_stream)
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
+    forms = []
+    for _ in range(7):
+        got = torch.empty(n, dtype=torch.int32, device="cuda")
+        ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
+        torch.cuda.synchronize()
+        assert ac.kernel_last == pm.KIND_AC
+        forms.append(ac.dfa_form_last)
+        assert torch.equal(got, want)
+    assert forms[:4] == [1, 1, 2, 2] and forms[4] == forms[5] == forms[6] in (1, 2), forms
+    ac.reset()  # a new stream: the forms are timed again
+    ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
+    torch.cuda.synchronize()
+    assert ac.dfa_form_last == 1 and torch.equal(got, want)
 
 
 def test_auto_count_only_follows_deep_walks():

@@ -9,7 +9,7 @@ import pytest
 
 import patternmatching_amd as pm
 from oracle_lib import DATA, GOLDEN, dict_paths, oracle_for
-from table_emulator import FlatImage, dfa_scan, filter2_maybe, filter_maybe, gid_to_code, rt_scan
+from table_emulator import FlatImage, dfa_scan, filter2_maybe, filter_maybe, gid_to_code, rt_scan, sdfa_scan
 
 MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
 SHIP = np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8)
@@ -121,12 +121,24 @@ def test_parent_and_depth_tables_follow_the_patterns_tree(key):
     assert depth.max() >= 3
 
 
+def section_offset(raw, tag):
+    """Byte offset of section `tag`'s data in a cached image file
+    (pm_flatten.cpp save(): 24-B header, then {tag u32, elem u32, n u64, data})."""
+    off = 24
+    while off < len(raw):
+        t, es, n = np.frombuffer(bytes(raw[off:off + 16]), np.uint32, 2).tolist() + [int.from_bytes(raw[off + 8:off + 16], "little")]
+        if t == tag:
+            return off + 16
+        off += 16 + es * n
+    raise KeyError(tag)
+
+
 def test_compiled_image_cache(tmp_path):
     """miss -> file written; hit -> identical tables; a
     truncated or foreign file is rebuilt; another dictionary gets its own file."""
     d = pm.Dictionary(dict_paths("et"))
     pats = d.patterns()
-    names = {pm.KIND_RT: ["t12", "filt", "t3h", "rec", "wide", "parent", "depth"], pm.KIND_AC: ["next", "out", "parent", "depth"]}
+    names = {pm.KIND_RT: ["t12", "filt", "t3h", "rec", "wide", "parent", "depth"], pm.KIND_AC: ["next", "out", "sblock", "sout", "parent", "depth"]}
     for kind, arrays in names.items():
         a = FlatImage(pats, kind, tmp_path)
         assert not a.cache_hit
@@ -139,7 +151,7 @@ def test_compiled_image_cache(tmp_path):
         # sizes intact, one value damaged: parent[P] = P (a cycle) -> rejected, rebuilt
         raw = bytearray(files[0].read_bytes())
         ngid = len(a.array("parent"))
-        off = len(raw) - (16 + 4 * ngid) - 4
+        off = section_offset(raw, 8) + 4 * (ngid - 1)
         raw[off:off + 4] = (ngid - 1).to_bytes(4, "little")
         files[0].write_bytes(bytes(raw))
         assert not FlatImage(pats, kind, tmp_path).cache_hit
@@ -165,8 +177,7 @@ def test_compiled_image_cache_rejects_a_damaged_filter(tmp_path):
     a = FlatImage(pats, pm.KIND_RT, tmp_path)
     (f,) = tmp_path.glob(f"pm-{pm.KIND_RT}-*.img")
     raw = bytearray(f.read_bytes())
-    # header 24 B; sections: 16-B header + data (scal 8 u32, t12 u16[65792], filt)
-    off = 24 + 16 + 32 + 16 + 2 * 65792 + 16
+    off = section_offset(raw, 3)  # filt
     filt = np.frombuffer(bytes(raw[off:off + 4 * 4096]), np.uint32)
     assert np.array_equal(filt, a.array("filt")[:4096])
     w = int(np.nonzero(filt)[0][0])
@@ -191,6 +202,8 @@ def test_duplicate_pattern_last_id_wins_and_caches(tmp_path):
         idx = img.array("index_of_gid")
         gids = rt_scan(img, text) if kind == pm.KIND_RT else dfa_scan(img, text)
         assert [int(idx[g]) if g else -1 for g in gids] == [-1, -1, -1, -1, 2, -1, -1, 3, -1, 1]
+        if kind == pm.KIND_AC:
+            assert np.array_equal(sdfa_scan(img, text), gids)
         parent, depth = img.array("parent"), img.array("depth")
         shadowed = int(np.nonzero(idx == 0)[0][1])  # gid of index 0 (idx[0] is the unused slot)
         assert parent[shadowed] == 0 and depth[shadowed] == 1
@@ -214,6 +227,22 @@ def test_dfa_image_ship_stream(key):
     d, img, tab = image(key, pm.KIND_AC)
     gold = np.fromfile(os.path.join(GOLDEN, f"ship_{key}.u32"), dtype="<u4")
     assert np.array_equal(tab[dfa_scan(img, SHIP)], gold)
+    assert np.array_equal(tab[sdfa_scan(img, SHIP)], gold)
+
+
+@pytest.mark.parametrize("key,mode", [("et", 0), ("snort", 1)])
+def test_sparse_dfa_image_random(key, mode):
+    """The sparse DFA form (records for states within PM_SDFA_K bytes of
+    their fallback's row) equals the oracle on random streams, and it is a
+    real reduction: most states are records."""
+    d, img, tab = image(key, pm.KIND_AC)
+    F = int(img.lib.pm_flat_dfa_sparse_rows(img.h))
+    S = len(img.array("sout"))
+    assert 1 <= F < S // 2
+    text = pm.gen_stream(1 << 16, seed=12, mode=mode)
+    o = oracle_for(key)
+    o.reset()
+    assert np.array_equal(tab[sdfa_scan(img, text)], o.scan_codes(text))
 
 
 def test_small_dictionaries():
@@ -248,3 +277,4 @@ def test_small_dictionaries():
                     break
         assert np.array_equal(tab[rt_scan(img, text)], exp), pats[:3]
         assert np.array_equal(dtab[dfa_scan(dimg, text)], exp), pats[:3]
+        assert np.array_equal(dtab[sdfa_scan(dimg, text)], exp), pats[:3]
