@@ -175,6 +175,10 @@ void pm_hip_debug_dfa_chains(int chains);
 void pm_hip_debug_dfa_sparse(int sparse);
 /* Timing sweeps only: positions per block of the sparse AC-DFA kernel (16 or 32; 0 = default). */
 void pm_hip_debug_dfa_block(int blk);
+/* Timing experiments only: variant of the sparse AC-DFA kernel for u32 ids
+ * (bit 0 non-temporal id stores, bit 1 non-temporal text loads, bit 2
+ * escapes looked up in the step loop, bit 3 64-position blocks; 0 = product). */
+void pm_hip_debug_dfa_variant(int v);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

@@ -56,6 +56,7 @@ void pm_dfa_set_min_seg(int min_seg);
 // default form is then the sparse one).
 void pm_dfa_set_sparse(int sparse);
 bool pm_dfa_forced_form();
+void pm_dfa_set_variant(int v);  // timing experiments of the sparse kernel (u32 ids, one chain)
 void pm_dfa_set_block(int blk);  // sparse form, one chain: positions per block (16 or 32)
 bool pm_dfa_default_sparse();  // the form a launch with DfaDev::form 0 runs
 // counts[0..4] += success, partial, false_neg, false_pos, all_matches of algo

@@ -1193,7 +1193,10 @@ __device__ __forceinline__ void sdfa_step(const uint8_t* __restrict__ base, uint
         if (miss[k]) v[k] = *reinterpret_cast<const uint32_t*>(base + q[k].w * 1024u + c[k] * 4u);
 }
 
-template <int OUTW, int CH, int BLK>
+// VAR (timing experiments, pm_dfa_set_variant): bit 0 = non-temporal id
+// stores, bit 1 = non-temporal text loads, bit 2 = escape lookups issued in
+// the step loop (no per-position state registers)
+template <int OUTW, int CH, int BLK, int VAR = 0>
 __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* __restrict__ text,
                                                                  int64_t stream_start, int64_t pos0, int64_t n,
                                                                  void* __restrict__ out,
@@ -1243,8 +1246,9 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* 
                 any |= act[k];
 #pragma unroll
                 for (int q = 0; q < BLK / 16; ++q) {
-                    const uint4 w = act[k] ? *reinterpret_cast<const uint4*>(text + lo[k] + BLK * b + 16 * q)
-                                           : make_uint4(0, 0, 0, 0);
+                    using v4 = __attribute__((ext_vector_type(4))) unsigned int;
+                    const v4* tp = reinterpret_cast<const v4*>(text + lo[k] + BLK * b + 16 * q);
+                    const v4 w = act[k] ? ((VAR & 2) ? __builtin_nontemporal_load(tp) : *tp) : v4{0u, 0u, 0u, 0u};
                     W[k][4 * q] = w.x; W[k][4 * q + 1] = w.y; W[k][4 * q + 2] = w.z; W[k][4 * q + 3] = w.w;
                 }
             }
@@ -1260,7 +1264,11 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* 
                 for (int k = 0; k < CH; ++k) {
                     s[k] = act[k] ? v[k] & DFA_STATE_MASK : s[k];
                     code[k][j] = v[k] >> 20;
-                    st[k][j] = s[k];
+                    if (VAR & 4) {
+                        if (code[k][j] == DFA_ESC) code[k][j] = outt[s[k]];
+                    } else {
+                        st[k][j] = s[k];
+                    }
                 }
             }
 #pragma unroll
@@ -1268,12 +1276,18 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* 
                 if (!act[k]) continue;
                 uint32_t r[BLK];
 #pragma unroll
-                for (int j = 0; j < BLK; ++j) r[j] = code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                for (int j = 0; j < BLK; ++j)
+                    r[j] = (VAR & 4) ? code[k][j] : code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
                 const int64_t i = lo[k] + BLK * b;
                 if (OUTW == 4) {
-                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
+                    using v4 = __attribute__((ext_vector_type(4))) unsigned int;
+                    v4* o = reinterpret_cast<v4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
 #pragma unroll
-                    for (int q = 0; q < BLK / 4; ++q) o[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+                    for (int q = 0; q < BLK / 4; ++q) {
+                        const v4 x = {r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
+                        if (VAR & 1) __builtin_nontemporal_store(x, o + q);
+                        else o[q] = x;
+                    }
                 }
                 if (OUTW == 2) {
                     uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + (i - pos0));
@@ -1551,6 +1565,7 @@ constexpr int DFA_CHAINS = 2, SDFA_CHAINS = 1;
 // 10.8 -> 9.7, ASCII 6.82 -> 6.15 at 512 lanes per CU; profiles/r02).
 constexpr int SDFA_BLK = 32;
 static int g_sdfa_blk = SDFA_BLK;
+static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64-position blocks)
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
 // does not name one (-1: not forced; the plugin then times both forms)
@@ -1568,7 +1583,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
-    const int64_t align = sparse && ch == 1 ? g_sdfa_blk : 16;  // whole blocks per segment
+    const int64_t align = sparse && ch == 1 ? ((g_sdfa_var & 8) ? 64 : g_sdfa_blk) : 16;  // whole blocks per segment
     seg = (seg + align - 1) / align * align;
     const int64_t nseg = (n + seg - 1) / seg;
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
@@ -1580,6 +1595,22 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                        t.sF, t.sout, t.warm, seg)
         if (ch == 2) {
             if (outw == 4) DS(4, 2, 16); else if (outw == 2) DS(2, 2, 16); else DS(0, 2, 16);
+        } else if (g_sdfa_var && outw == 4) {
+#define DV(V, B)                                                                                                  \
+    hipLaunchKernelGGL((dfa_sparse_kernel<4, 1, B, V>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.sbase, \
+                       t.sF, t.sout, t.warm, seg)
+            switch (g_sdfa_var) {
+                case 1: DV(1, 32); break;
+                case 2: DV(2, 32); break;
+                case 3: DV(3, 32); break;
+                case 4: DV(4, 32); break;
+                case 5: DV(5, 32); break;
+                case 7: DV(7, 32); break;
+                case 12: DV(4, 64); break;
+                case 13: DV(5, 64); break;
+                default: DV(0, 32); break;
+            }
+#undef DV
         } else if (g_sdfa_blk == 32) {
             if (outw == 4) DS(4, 1, 32); else if (outw == 2) DS(2, 1, 32); else DS(0, 1, 32);
         } else {
@@ -1612,6 +1643,7 @@ void pm_dfa_set_shape(int lanes_per_cu) { g_dfa_lanes_per_cu = lanes_per_cu > 0 
 void pm_dfa_set_min_seg(int min_seg) { g_dfa_min_seg = min_seg >= 16 ? min_seg : 0; }
 void pm_dfa_set_sparse(int sparse) { g_dfa_sparse = sparse < 0 ? -1 : sparse != 0; }
 void pm_dfa_set_block(int blk) { g_sdfa_blk = blk == 16 || blk == 32 ? blk : SDFA_BLK; }
+void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }

@@ -24,7 +24,8 @@ ap.add_argument("--lanes", default="256,512,1024")
 ap.add_argument("--streams", default="ascii,ship,lines")
 ap.add_argument("--forms", default="0,1", help="0 = dense rows, 1 = sparse rows + records (pm_hip_debug_dfa_sparse)")
 ap.add_argument("--chains", default="1,2")
-ap.add_argument("--blocks", default="16", help="sparse form, one chain: positions per block (16,32)")
+ap.add_argument("--blocks", default="32", help="sparse form, one chain: positions per block (16,32)")
+ap.add_argument("--variants", default="0", help="sparse form, one chain: kernel variants (pm_hip_debug_dfa_variant)")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 data = os.path.join(REPO, "tests", "golden", "data")
@@ -69,17 +70,20 @@ for stream in args.streams.split(","):
             lib.pm_hip_debug_dfa_shape(lanes)
             for ch in [int(x) for x in args.chains.split(",")]:
                 lib.pm_hip_debug_dfa_chains(ch)
-                for blk in [int(x) for x in args.blocks.split(",")] if form and ch == 1 else [16]:
+                combos = [(b, v) for b in map(int, args.blocks.split(",")) for v in map(int, args.variants.split(","))]
+                for blk, var in combos if form and ch == 1 else [(0, 0)]:
                     lib.pm_hip_debug_dfa_block(blk)
+                    lib.pm_hip_debug_dfa_variant(var)
                     dst = ref if first else out
                     ms = timed(lambda: m.scan_device(text.data_ptr(), 0, 0, n, dst.data_ptr(), None, s.cuda_stream))
                     same = True if first else bool(torch.equal(out, ref))
                     first = False
-                    key = f"{stream}/{'sparse' if form else 'dense'}/L{lanes}/ch{ch}/b{blk}"
+                    key = f"{stream}/{'sparse' if form else 'dense'}/L{lanes}/ch{ch}/b{blk}/v{var}"
                     res[key] = {"ms": round(ms, 4), "GBps": round(n / ms / 1e6, 1), "same": same}
                     print(key, res[key], flush=True)
 lib.pm_hip_debug_dfa_shape(0)
 lib.pm_hip_debug_dfa_chains(0)
 lib.pm_hip_debug_dfa_sparse(-1)
 lib.pm_hip_debug_dfa_block(0)
+lib.pm_hip_debug_dfa_variant(0)
 print(json.dumps(res))
