@@ -61,8 +61,9 @@ def write_dict(tmp_path, seed, data):
 
 @pytest.mark.parametrize("seed", range(12))
 def test_fuzz_images_cpu(tmp_path, seed):
-    """The RT and DFA images (emulated on the CPU) equal the oracle."""
-    from table_emulator import FlatImage, dfa_scan, gid_to_code, rt_scan
+    """The RT image and both forms of the DFA image (emulated on the CPU)
+    equal the oracle."""
+    from table_emulator import FlatImage, dfa_scan, gid_to_code, rt_scan, sdfa_scan
     data, text = fuzz_case(seed, 6000)
     path = write_dict(tmp_path, seed, data)
     o = Oracle([path])
@@ -76,6 +77,8 @@ def test_fuzz_images_cpu(tmp_path, seed):
         tab = gid_to_code(img, d)
         got = tab[rt_scan(img, text)] if kind == pm.KIND_RT else tab[dfa_scan(img, text)]
         assert np.array_equal(got, exp), (seed, kind)
+        if kind == pm.KIND_AC:
+            assert np.array_equal(tab[sdfa_scan(img, text)], exp), (seed, "sparse")
 
 
 @pytest.mark.gpu
