@@ -16,15 +16,16 @@ src = os.path.join(REPO, "gpurun_out", f"round_{tag}")
 os.makedirs(dst, exist_ok=True)
 names = {"dense": "C3 snort 1 GiB dense_u32 (bench default, 16-core reference baseline)",
          "dense16": "snort 1 GiB dense_u16", "count": "snort 1 GiB count_only",
-         "ac": "snort 1 GiB AC dense DFA (reliable instance), dense_u32",
+         "ac": "snort 1 GiB AC-DFA (reliable instance; the faster of its two forms, timed), dense_u32",
          "c2_et64m": "C2 et 64 MiB dense_u32", "c5_merged4g": "C5 merged 4 GiB dense_u32",
          "score": "snort 1 GiB dense_u32 + on-device accuracy scoring vs the AC instance (--score)",
          "ship": "snort, the shipped stream tiled to 1 GiB (deep matches), dense_u32",
          "ship_count": "snort, the shipped stream tiled to 1 GiB, count_only",
-         "ship_ac": "snort, the shipped stream tiled to 1 GiB, AC dense DFA, dense_u32",
-         "ship_auto": "snort, the shipped stream tiled to 1 GiB, auto kind (RT, then AC after a spilling launch), dense_u32",
+         "ship_ac": "snort, the shipped stream tiled to 1 GiB, AC-DFA (forms timed), dense_u32",
+         "ship_auto": "snort, the shipped stream tiled to 1 GiB, auto kind (RT, then timed AC forms after a spilling launch), dense_u32",
          "lines": "snort, the lines stream (random dictionary patterns, no period), 1 GiB, RT, dense_u32",
-         "lines_ac": "snort, the lines stream, 1 GiB, AC dense DFA (output-coded), dense_u32"}
+         "lines_ac": "snort, the lines stream, 1 GiB, AC-DFA (forms timed: rows + records), dense_u32",
+         "lines_auto": "snort, the lines stream, 1 GiB, auto kind, dense_u32"}
 lines = {}
 for k, label in names.items():
     p = os.path.join(src, f"bench_{k}.json")
@@ -35,6 +36,9 @@ json.dump(lines, open(os.path.join(dst, f"bench_{rnd}.json"), "w"), indent=1)
 shutil.copy(os.path.join(src, "prof", "bench_kernel_stats.csv"),
             os.path.join(dst, "rt_dense_snort_1GiB_kernel_stats.csv"))
 shutil.copy(os.path.join(src, "pytest_gpu.log"), os.path.join(dst, f"pytest_gpu_{rnd}.log"))
+la = os.path.join(src, "prof_lines_ac", "bench_kernel_stats.csv")
+if os.path.exists(la):
+    shutil.copy(la, os.path.join(dst, "ac_lines_snort_1GiB_kernel_stats.csv"))
 pmc = json.load(open(os.path.join(src, "pmc_summary.json")))
 json.dump(pmc, open(os.path.join(dst, "rt_dense_snort_1GiB_pmc_traffic.json"), "w"), indent=1)
 tr_path = os.path.join(REPO, "profiles", "traffic.json")

@@ -30,9 +30,12 @@ run ship_ac --stream ship --kernel ac --no-cpu --steps 5
 run ship_auto --stream ship --kernel auto --no-cpu --steps 5
 run lines --stream lines --no-cpu --steps 5
 run lines_ac --stream lines --kernel ac --no-cpu --steps 5
+run lines_auto --stream lines --kernel auto --no-cpu --steps 5
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
     python3 "$ROOT/bench.py" --no-cpu --steps 10 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail "$OUT/bench_prof.err"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_lines_ac" -o bench -- \
+    python3 "$ROOT/bench.py" --no-cpu --steps 5 --stream lines --kernel ac > "$OUT/bench_prof_lines_ac.json" 2> "$OUT/bench_prof_lines_ac.err" || { tail "$OUT/bench_prof_lines_ac.err"; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d "$OUT/pmc/$c" -o c -- \
     python3 "$ROOT/bench.py" --no-cpu --steps 3 --warmup 1 > "$OUT/pmc_$c.log" 2>&1 || { tail "$OUT/pmc_$c.log"; exit 1; }
