@@ -1172,7 +1172,7 @@ __device__ __forceinline__ uint32_t sdfa_off(uint32_t s, uint32_t c, uint32_t F)
     return s < F ? s * 1024u + (c & 0xFCu) * 4u : s * 16u + F * 1008u;  // F*1024 + (s-F)*16
 }
 
-template <int CH>
+template <int CH, bool kNoMiss = false>
 __device__ __forceinline__ void sdfa_step(const uint8_t* __restrict__ base, uint32_t F, const uint32_t (&s)[CH],
                                           const uint32_t (&c)[CH], uint32_t (&v)[CH]) {
     uint4 q[CH];
@@ -1188,6 +1188,11 @@ __device__ __forceinline__ void sdfa_step(const uint8_t* __restrict__ base, uint
         v[k] = isrow ? rowv : (h0 ? q[k].y : q[k].z);
         miss[k] = !isrow && !h0 && !h1;
     }
+    if (kNoMiss) {  // timing ablation only: a miss goes to the root (wrong ids, every state in range)
+#pragma unroll
+        for (int k = 0; k < CH; ++k) v[k] = miss[k] ? 0u : v[k];
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < CH; ++k)
         if (miss[k]) v[k] = *reinterpret_cast<const uint32_t*>(base + q[k].w * 1024u + c[k] * 4u);
@@ -1195,7 +1200,9 @@ __device__ __forceinline__ void sdfa_step(const uint8_t* __restrict__ base, uint
 
 // VAR (timing experiments, pm_dfa_set_variant): bit 0 = non-temporal id
 // stores, bit 1 = non-temporal text loads, bit 2 = escape lookups issued in
-// the step loop (no per-position state registers)
+// the step loop (no per-position state registers), bit 3 = no second load
+// at a record miss (ablation: wrong ids, timing only), bit 4 = no escape
+// lookups (ablation: ids >= 4095 read as 4095, timing only)
 template <int OUTW, int CH, int BLK, int VAR = 0>
 __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* __restrict__ text,
                                                                  int64_t stream_start, int64_t pos0, int64_t n,
@@ -1259,7 +1266,7 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* 
                 uint32_t c[CH], v[CH];
 #pragma unroll
                 for (int k = 0; k < CH; ++k) c[k] = (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                sdfa_step<CH>(base, F, s, c, v);
+                sdfa_step<CH, (VAR & 8) != 0>(base, F, s, c, v);
 #pragma unroll
                 for (int k = 0; k < CH; ++k) {
                     s[k] = act[k] ? v[k] & DFA_STATE_MASK : s[k];
@@ -1277,7 +1284,7 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* 
                 uint32_t r[BLK];
 #pragma unroll
                 for (int j = 0; j < BLK; ++j)
-                    r[j] = (VAR & 4) ? code[k][j] : code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                    r[j] = (VAR & 4) || (VAR & 16) ? code[k][j] : code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
                 const int64_t i = lo[k] + BLK * b;
                 if (OUTW == 4) {
                     using v4 = __attribute__((ext_vector_type(4))) unsigned int;
@@ -1608,6 +1615,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                 case 7: DV(7, 32); break;
                 case 12: DV(4, 64); break;
                 case 13: DV(5, 64); break;
+                case 16: DV(8, 32); break;
+                case 32: DV(16, 32); break;
+                case 48: DV(24, 32); break;
                 default: DV(0, 32); break;
             }
 #undef DV
