@@ -1072,7 +1072,7 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
 constexpr uint32_t DFA_STATE_MASK = 0xFFFFFu;  // must match pm_flatten.h
 constexpr uint32_t DFA_ESC = 4095u;
 
-template <int OUTW, int CH>
+template <int OUTW, int CH, int BLK = 16>
 __global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
                                                                 int64_t pos0, int64_t n, void* __restrict__ out,
                                                                 unsigned long long* __restrict__ count,
@@ -1096,22 +1096,26 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* _
             if (sg < nseg)
                 for (int64_t i = wlo; i < lo[k]; ++i) s[k] = nxt[(size_t)s[k] * 256 + text[i]] & DFA_STATE_MASK;
         }
-        const int64_t nblk = seg_len / 16;
+        const int64_t nblk = seg_len / BLK;
         for (int64_t b = 0; b < nblk; ++b) {
             bool act[CH];
-            uint32_t W[CH][4];
+            uint32_t W[CH][BLK / 4];
             bool any = false;
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
-                act[k] = lo[k] + 16 * b + 16 <= hi[k];
+                act[k] = lo[k] + BLK * b + BLK <= hi[k];
                 any |= act[k];
-                const uint4 w = act[k] ? *reinterpret_cast<const uint4*>(text + lo[k] + 16 * b) : make_uint4(0, 0, 0, 0);
-                W[k][0] = w.x; W[k][1] = w.y; W[k][2] = w.z; W[k][3] = w.w;
+#pragma unroll
+                for (int q = 0; q < BLK / 16; ++q) {
+                    const uint4 w = act[k] ? *reinterpret_cast<const uint4*>(text + lo[k] + BLK * b + 16 * q)
+                                           : make_uint4(0, 0, 0, 0);
+                    W[k][4 * q] = w.x; W[k][4 * q + 1] = w.y; W[k][4 * q + 2] = w.z; W[k][4 * q + 3] = w.w;
+                }
             }
             if (!any) break;
-            uint32_t code[CH][16], st[CH][16];
+            uint32_t code[CH][BLK], st[CH][BLK];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
+            for (int j = 0; j < BLK; ++j) {
 #pragma unroll
                 for (int k = 0; k < CH; ++k) {
                     const uint32_t c = (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu;
@@ -1124,29 +1128,29 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* _
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
                 if (!act[k]) continue;
-                uint32_t r[16];
+                uint32_t r[BLK];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) r[j] = code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
-                const int64_t i = lo[k] + 16 * b;
+                for (int j = 0; j < BLK; ++j) r[j] = code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                const int64_t i = lo[k] + BLK * b;
                 if (OUTW == 4) {
                     uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
-                    o[0] = make_uint4(r[0], r[1], r[2], r[3]);
-                    o[1] = make_uint4(r[4], r[5], r[6], r[7]);
-                    o[2] = make_uint4(r[8], r[9], r[10], r[11]);
-                    o[3] = make_uint4(r[12], r[13], r[14], r[15]);
+#pragma unroll
+                    for (int q = 0; q < BLK / 4; ++q) o[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
                 }
                 if (OUTW == 2) {
                     uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + (i - pos0));
-                    o[0] = make_uint4(r[0] | r[1] << 16, r[2] | r[3] << 16, r[4] | r[5] << 16, r[6] | r[7] << 16);
-                    o[1] = make_uint4(r[8] | r[9] << 16, r[10] | r[11] << 16, r[12] | r[13] << 16, r[14] | r[15] << 16);
+#pragma unroll
+                    for (int q = 0; q < BLK / 8; ++q)
+                        o[q] = make_uint4(r[8 * q] | r[8 * q + 1] << 16, r[8 * q + 2] | r[8 * q + 3] << 16,
+                                          r[8 * q + 4] | r[8 * q + 5] << 16, r[8 * q + 6] | r[8 * q + 7] << 16);
                 }
 #pragma unroll
-                for (int j = 0; j < 16; ++j) cnt += r[j] != 0u;
+                for (int j = 0; j < BLK; ++j) cnt += r[j] != 0u;
             }
         }
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
-            for (int64_t i = lo[k] + 16 * ((hi[k] - lo[k]) / 16); i < hi[k]; ++i) {
+            for (int64_t i = lo[k] + BLK * ((hi[k] - lo[k]) / BLK); i < hi[k]; ++i) {
                 s[k] = nxt[(size_t)s[k] * 256 + text[i]] & DFA_STATE_MASK;
                 const uint32_t v = outt[s[k]];
                 if (OUTW) put_id<OUTW>(out, i - pos0, v);
@@ -1572,6 +1576,7 @@ constexpr int DFA_CHAINS = 2, SDFA_CHAINS = 1;
 // 10.8 -> 9.7, ASCII 6.82 -> 6.15 at 512 lanes per CU; profiles/r02).
 constexpr int SDFA_BLK = 32;
 static int g_sdfa_blk = SDFA_BLK;
+static int g_dfa_dense_blk = 16;  // dense coded kernel, u32 ids (16 or 32; pm_dfa_set_block with a form forced dense)
 static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64-position blocks)
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
@@ -1590,7 +1595,8 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
-    const int64_t align = sparse && ch == 1 ? ((g_sdfa_var & 8) ? 64 : g_sdfa_blk) : 16;  // whole blocks per segment
+    const int64_t align = sparse && ch == 1 ? ((g_sdfa_var & 8) ? 64 : g_sdfa_blk)
+                          : (!sparse && t.coded && outw == 4 ? g_dfa_dense_blk : 16);  // whole blocks per segment
     seg = (seg + align - 1) / align * align;
     const int64_t nseg = (n + seg - 1) / seg;
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
@@ -1632,7 +1638,14 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (t.coded) {
 #define DC(W, C) \
     hipLaunchKernelGGL((dfa_coded_kernel<W, C>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, t.out, t.warm, seg)
-        if (ch == 2) {
+        if (g_dfa_dense_blk == 32 && outw == 4) {  // timing experiment (pm_dfa_set_block)
+            if (ch == 2)
+                hipLaunchKernelGGL((dfa_coded_kernel<4, 2, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count,
+                                   t.next, t.out, t.warm, seg);
+            else
+                hipLaunchKernelGGL((dfa_coded_kernel<4, 1, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count,
+                                   t.next, t.out, t.warm, seg);
+        } else if (ch == 2) {
             if (outw == 4) DC(4, 2); else if (outw == 2) DC(2, 2); else DC(0, 2);
         } else {
             if (outw == 4) DC(4, 1); else if (outw == 2) DC(2, 1); else DC(0, 1);
@@ -1652,7 +1665,10 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 void pm_dfa_set_shape(int lanes_per_cu) { g_dfa_lanes_per_cu = lanes_per_cu > 0 ? lanes_per_cu : DFA_LANES_PER_CU; }
 void pm_dfa_set_min_seg(int min_seg) { g_dfa_min_seg = min_seg >= 16 ? min_seg : 0; }
 void pm_dfa_set_sparse(int sparse) { g_dfa_sparse = sparse < 0 ? -1 : sparse != 0; }
-void pm_dfa_set_block(int blk) { g_sdfa_blk = blk == 16 || blk == 32 ? blk : SDFA_BLK; }
+void pm_dfa_set_block(int blk) {
+    g_sdfa_blk = blk == 16 || blk == 32 ? blk : SDFA_BLK;
+    g_dfa_dense_blk = blk == 32 ? 32 : 16;
+}
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }

@@ -25,6 +25,7 @@ ap.add_argument("--streams", default="ascii,ship,lines")
 ap.add_argument("--forms", default="0,1", help="0 = dense rows, 1 = sparse rows + records (pm_hip_debug_dfa_sparse)")
 ap.add_argument("--chains", default="1,2")
 ap.add_argument("--blocks", default="32", help="sparse form, one chain: positions per block (16,32)")
+ap.add_argument("--dense-blocks", default="0", help="dense form: positions per block (16,32; 0 = default)")
 ap.add_argument("--variants", default="0", help="sparse form, one chain: kernel variants (pm_hip_debug_dfa_variant)")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
@@ -71,7 +72,7 @@ for stream in args.streams.split(","):
             for ch in [int(x) for x in args.chains.split(",")]:
                 lib.pm_hip_debug_dfa_chains(ch)
                 combos = [(b, v) for b in map(int, args.blocks.split(",")) for v in map(int, args.variants.split(","))]
-                for blk, var in combos if form and ch == 1 else [(0, 0)]:
+                for blk, var in combos if form and ch == 1 else [(b, 0) for b in map(int, args.dense_blocks.split(","))]:
                     lib.pm_hip_debug_dfa_block(blk)
                     lib.pm_hip_debug_dfa_variant(var)
                     dst = ref if first else out

@@ -625,8 +625,9 @@ def test_lines_stream_generator_and_kernels():
     assert np.array_equal(o.scan_codes(host), rt._codes[a[: 1 << 20].cpu().numpy().view(np.uint32)])
 
 
-@pytest.mark.parametrize("stream", ["ascii", "lines", "ship"])
-def test_sparse_dfa_equals_dense_dfa(stream):
+@pytest.mark.parametrize("key,stream", [("snort", "ascii"), ("snort", "lines"), ("snort", "ship"),
+                                        ("et", "lines"), ("merged", "lines"), ("merged", "ship")])
+def test_sparse_dfa_equals_dense_dfa(key, stream):
     """The AC kind's two forms of the output-coded automaton -- dense rows
     (dfa_coded_kernel) and rows + default-transition records
     (dfa_sparse_kernel, pm_flatten.h) -- give the same u32 / u16 ids and
@@ -634,8 +635,8 @@ def test_sparse_dfa_equals_dense_dfa(stream):
     warm-up to 64 MiB, and equal the RT kernel."""
     torch = _torch()
     lib = pm.load()
-    rt, ac = matcher("snort", "rt"), matcher("snort", "ac")
-    n = 64 << 20
+    rt, ac = matcher(key, "rt"), matcher(key, "ac")
+    n = (64 if key == "snort" else 16) << 20
     s = torch.cuda.current_stream().cuda_stream
     dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     if stream == "ascii":

@@ -222,7 +222,7 @@ def test_rt_image_context():
         assert np.array_equal(got, full[start:start + 3000])
 
 
-@pytest.mark.parametrize("key", ["et"])
+@pytest.mark.parametrize("key", ["et", "snort", "merged"])
 def test_dfa_image_ship_stream(key):
     d, img, tab = image(key, pm.KIND_AC)
     gold = np.fromfile(os.path.join(GOLDEN, f"ship_{key}.u32"), dtype="<u4")
