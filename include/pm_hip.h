@@ -173,7 +173,8 @@ void pm_hip_debug_dfa_chains(int chains);
  * (rows + 16-B default-transition records, pm_flatten.h), 0 = dense rows,
  * -1 = default. */
 void pm_hip_debug_dfa_sparse(int sparse);
-/* Timing sweeps only: positions per block of the sparse AC-DFA kernel (16 or 32; 0 = default). */
+/* Timing sweeps only: positions per block of both AC-DFA kernels (16 or 32;
+ * 0 = the defaults). */
 void pm_hip_debug_dfa_block(int blk);
 /* Timing experiments only: variant of the sparse AC-DFA kernel for u32 ids
  * (bit 0 non-temporal id stores, bit 1 non-temporal text loads, bit 2

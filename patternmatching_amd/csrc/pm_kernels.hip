@@ -1576,7 +1576,12 @@ constexpr int DFA_CHAINS = 2, SDFA_CHAINS = 1;
 // 10.8 -> 9.7, ASCII 6.82 -> 6.15 at 512 lanes per CU; profiles/r02).
 constexpr int SDFA_BLK = 32;
 static int g_sdfa_blk = SDFA_BLK;
-static int g_dfa_dense_blk = 16;  // dense coded kernel, u32 ids (16 or 32; pm_dfa_set_block with a form forced dense)
+// The dense coded kernel with u32 ids: 32 positions per block (one whole
+// 128-B line of ids per lane and segment) measured faster at every shape:
+// shipped stream 4.32 -> 3.84 ms, ASCII 6.58 -> 5.93, lines 20.5 -> 19.8 at
+// 512 lanes x 2 segments (profiles/r02/dfa_dense_block_sweep.txt).
+constexpr int DFA_DENSE_BLK = 32;
+static int g_dfa_dense_blk = DFA_DENSE_BLK;
 static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64-position blocks)
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
@@ -1595,7 +1600,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
-    const int64_t align = sparse && ch == 1 ? ((g_sdfa_var & 8) ? 64 : g_sdfa_blk)
+    const int64_t align = sparse && (ch == 1 || outw == 4) ? ((g_sdfa_var & 8) ? 64 : g_sdfa_blk)
                           : (!sparse && t.coded && outw == 4 ? g_dfa_dense_blk : 16);  // whole blocks per segment
     seg = (seg + align - 1) / align * align;
     const int64_t nseg = (n + seg - 1) / seg;
@@ -1607,7 +1612,8 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     hipLaunchKernelGGL((dfa_sparse_kernel<W, C, B>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.sbase, \
                        t.sF, t.sout, t.warm, seg)
         if (ch == 2) {
-            if (outw == 4) DS(4, 2, 16); else if (outw == 2) DS(2, 2, 16); else DS(0, 2, 16);
+            if (outw == 4 && g_sdfa_blk == 32) DS(4, 2, 32);
+            else if (outw == 4) DS(4, 2, 16); else if (outw == 2) DS(2, 2, 16); else DS(0, 2, 16);
         } else if (g_sdfa_var && outw == 4) {
 #define DV(V, B)                                                                                                  \
     hipLaunchKernelGGL((dfa_sparse_kernel<4, 1, B, V>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.sbase, \
@@ -1638,7 +1644,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (t.coded) {
 #define DC(W, C) \
     hipLaunchKernelGGL((dfa_coded_kernel<W, C>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, t.out, t.warm, seg)
-        if (g_dfa_dense_blk == 32 && outw == 4) {  // timing experiment (pm_dfa_set_block)
+        if (g_dfa_dense_blk == 32 && outw == 4) {
             if (ch == 2)
                 hipLaunchKernelGGL((dfa_coded_kernel<4, 2, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count,
                                    t.next, t.out, t.warm, seg);
@@ -1667,7 +1673,7 @@ void pm_dfa_set_min_seg(int min_seg) { g_dfa_min_seg = min_seg >= 16 ? min_seg :
 void pm_dfa_set_sparse(int sparse) { g_dfa_sparse = sparse < 0 ? -1 : sparse != 0; }
 void pm_dfa_set_block(int blk) {
     g_sdfa_blk = blk == 16 || blk == 32 ? blk : SDFA_BLK;
-    g_dfa_dense_blk = blk == 32 ? 32 : 16;
+    g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }

@@ -651,7 +651,7 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
         for size, start in ((n, 0), (1000, 5000), (100 << 10, 12345), (3 << 20, 1 << 20)):
             start &= ~15
             got = {}
-            for sparse, blk in ((0, 16), (1, 16), (1, 32)):
+            for sparse, blk in ((0, 16), (0, 32), (1, 16), (1, 32)):
                 lib.pm_hip_debug_dfa_sparse(sparse)
                 lib.pm_hip_debug_dfa_block(blk)
                 a = torch.zeros(size, dtype=torch.int32, device="cuda")
@@ -663,7 +663,7 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
                 torch.cuda.synchronize()
                 got[(sparse, blk)] = (a, h, c)
             a0, h0, c0 = got[(0, 16)]
-            for key in ((1, 16), (1, 32)):
+            for key in ((0, 32), (1, 16), (1, 32)):
                 a1, h1, c1 = got[key]
                 assert torch.equal(a0, a1) and torch.equal(h0, h1) and torch.equal(c0, c1), key
             assert torch.equal(a1, ref[start:start + size])
