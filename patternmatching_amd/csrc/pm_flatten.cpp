@@ -359,26 +359,42 @@ PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap&
 // failure (shallower) is decided before it.  The fallback of v is fail[v]
 // when that keeps a row, else fail[v]'s own fallback; then delta(v, c) =
 // next[v][c] = next[fallback][c] except at the bytes where the two rows
-// differ, and v becomes a record when those are at most PM_SDFA_K.
-static void build_sparse(DfaImage& im, const std::vector<uint32_t>& fail, const std::vector<uint32_t>& order) {
+// differ, and v becomes a record when those are at most PM_SDFA_K.  That
+// set needs no row scan: row(v) differs from row(fail[v]) exactly at v's
+// goto bytes (a child is one level deeper than any state on the other row),
+// and row(fail[v]) from the fallback's row at fail[v]'s own set, so
+// D(v) = children(v) | D(fail[v]) when fail[v] is a record, children(v)
+// when it keeps a row.
+static void build_sparse(DfaImage& im, const BfsTrie& t, const std::vector<uint32_t>& fail,
+                         const std::vector<uint32_t>& order) {
     const uint32_t S = im.states;
     std::vector<uint32_t> fb(S, UINT32_MAX);  // fallback (old numbering) of a record; UINT32_MAX = row
-    std::vector<uint32_t> slots(S, 0);         // record x word (bytes still in the old numbering's row)
+    std::vector<uint32_t> slots(S, 0);         // record x word: its D bytes, ascending
     for (uint32_t v : order) {
-        if (v == 0) continue;
-        const uint32_t f = fb[fail[v]] == UINT32_MAX ? fail[v] : fb[fail[v]];
-        const uint32_t* a = &im.next[(size_t)v * 256];
-        const uint32_t* b = &im.next[(size_t)f * 256];
-        uint32_t nd = 0, x = 0;
-        for (uint32_t c = 0; c < 256 && nd <= PM_SDFA_K; ++c)
-            if (a[c] != b[c]) {
-                if (nd < PM_SDFA_K) x |= (c | 0x100u) << (16 * nd);
-                ++nd;
+        if (v == 0 || t.ccount[v] > PM_SDFA_K) continue;
+        const uint32_t u = fail[v];
+        uint32_t d[PM_SDFA_K + 1], nd = 0;
+        for (uint32_t k = 0; k < t.ccount[v]; ++k) d[nd++] = t.label[t.cstart[v] + k];
+        if (fb[u] != UINT32_MAX)  // fail[v] is a record: add its bytes not already there
+            for (uint32_t q = 0; q < PM_SDFA_K; ++q) {
+                const uint32_t x = slots[u] >> (16 * q);
+                if (!(x & 0x100u)) continue;
+                const uint32_t c = x & 0xFFu;
+                bool have = false;
+                for (uint32_t k = 0; k < nd; ++k) have |= d[k] == c;
+                if (have) continue;
+                if (nd == PM_SDFA_K) {
+                    nd = PM_SDFA_K + 1;
+                    break;
+                }
+                d[nd++] = c;
             }
-        if (nd <= PM_SDFA_K) {
-            fb[v] = f;
-            slots[v] = x;
-        }
+        if (nd > PM_SDFA_K) continue;
+        std::sort(d, d + nd);
+        uint32_t x = 0;
+        for (uint32_t k = 0; k < nd; ++k) x |= (d[k] | 0x100u) << (16 * k);
+        fb[v] = fb[u] == UINT32_MAX ? u : fb[u];
+        slots[v] = x;
     }
     // new ids in the trie's own order (depth-first below PM_DFA_DFS_DEPTH):
     // the records of a unary run of states are then consecutive 16-B
@@ -446,7 +462,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
     // output-coded transitions (pm_flatten.h): target | code << 20
     if (pm_dfa_coded(S)) {
         for (uint32_t& x : im.next) x |= std::min(im.out[x], PM_DFA_ESC) << 20;
-        build_sparse(im, fail, by_depth);
+        build_sparse(im, t, fail, by_depth);
     }
     return im;
 }
