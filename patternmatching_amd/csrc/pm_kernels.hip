@@ -34,6 +34,13 @@
 //   lock step when coded), started from the root max_len-1 bytes before the
 //   segment (SURVEY.md §0.1 shard rule), so every segment is independent
 //   and exact.
+//
+// dfa_sparse_kernel  the same automaton in its sparse form: full rows only
+//   for states whose row differs from their fallback's in more than two
+//   bytes, 16-B default-transition records for the rest (pm_flatten.h).  A
+//   step is one 16-B load (a row's quad, or the record) plus, at a record
+//   whose two bytes miss, one 4-B load of the fallback's row.  The plugin
+//   times both forms and keeps the faster per input (pm_plugin.hip).
 #include <type_traits>
 
 #include <algorithm>
