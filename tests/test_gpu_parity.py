@@ -551,6 +551,16 @@ def test_full_size_binary_and_deep_streams_kernels_agree(stream):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert int(ca.item()) == int(cb.item()) == int((a != 0).sum().item())
+    lib = pm.load()
+    try:  # both DFA forms at full size
+        for form in (0, 1):
+            lib.pm_hip_debug_dfa_sparse(form)
+            b.zero_()
+            ac.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), None, s)
+            torch.cuda.synchronize()
+            assert ac.dfa_form_last == 1 + form and torch.equal(a, b), form
+    finally:
+        lib.pm_hip_debug_dfa_sparse(-1)
     for _ in range(2):  # auto: an RT launch, then (deep stream) the DFA
         b.zero_()
         au.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), None, s)
