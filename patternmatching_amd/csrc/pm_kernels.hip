@@ -1589,6 +1589,7 @@ static int g_sdfa_blk = SDFA_BLK;
 // 512 lanes x 2 segments (profiles/r02/dfa_dense_block_sweep.txt).
 constexpr int DFA_DENSE_BLK = 32;
 static int g_dfa_dense_blk = DFA_DENSE_BLK;
+static int g_dfa_dense_blk16 = 16;  // the same for u16 ids (timing experiment: pm_dfa_set_variant 64 -> 32)
 static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64-position blocks)
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
@@ -1608,7 +1609,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
     const int64_t align = sparse && (ch == 1 || outw == 4) ? ((g_sdfa_var & 8) ? 64 : g_sdfa_blk)
-                          : (!sparse && t.coded && outw == 4 ? g_dfa_dense_blk : 16);  // whole blocks per segment
+                          : !sparse && t.coded && outw == 4 ? g_dfa_dense_blk
+                          : !sparse && t.coded && outw == 2 && ch == 2 ? g_dfa_dense_blk16
+                                                                       : 16;  // whole blocks per segment
     seg = (seg + align - 1) / align * align;
     const int64_t nseg = (n + seg - 1) / seg;
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
@@ -1658,6 +1661,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             else
                 hipLaunchKernelGGL((dfa_coded_kernel<4, 1, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count,
                                    t.next, t.out, t.warm, seg);
+        } else if (g_dfa_dense_blk16 == 32 && outw == 2 && ch == 2) {  // timing experiment (pm_dfa_set_variant 64)
+            hipLaunchKernelGGL((dfa_coded_kernel<2, 2, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count,
+                               t.next, t.out, t.warm, seg);
         } else if (ch == 2) {
             if (outw == 4) DC(4, 2); else if (outw == 2) DC(2, 2); else DC(0, 2);
         } else {
@@ -1682,7 +1688,10 @@ void pm_dfa_set_block(int blk) {
     g_sdfa_blk = blk == 16 || blk == 32 ? blk : SDFA_BLK;
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
-void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
+void pm_dfa_set_variant(int v) {
+    g_sdfa_var = v & 63;
+    g_dfa_dense_blk16 = (v & 64) ? 32 : 16;
+}
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }

@@ -25,6 +25,7 @@ ap.add_argument("--streams", default="ascii,ship,lines")
 ap.add_argument("--forms", default="0,1", help="0 = dense rows, 1 = sparse rows + records (pm_hip_debug_dfa_sparse)")
 ap.add_argument("--chains", default="1,2")
 ap.add_argument("--blocks", default="32", help="sparse form, one chain: positions per block (16,32)")
+ap.add_argument("--width", type=int, default=4, choices=[2, 4], help="id width of the timed launches")
 ap.add_argument("--dense-blocks", default="0", help="dense form: positions per block (16,32; 0 = default)")
 ap.add_argument("--variants", default="0", help="sparse form, one chain: kernel variants (pm_hip_debug_dfa_variant)")
 args = ap.parse_args()
@@ -38,8 +39,8 @@ m.compile()
 n = args.bytes
 s = torch.cuda.current_stream()
 text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-ref = torch.empty(n, dtype=torch.int32, device="cuda")
-out = torch.empty(n, dtype=torch.int32, device="cuda")
+ref = torch.empty(n, dtype=torch.int32 if args.width == 4 else torch.int16, device="cuda")
+out = torch.empty_like(ref)
 res = {}
 
 
@@ -72,11 +73,13 @@ for stream in args.streams.split(","):
             for ch in [int(x) for x in args.chains.split(",")]:
                 lib.pm_hip_debug_dfa_chains(ch)
                 combos = [(b, v) for b in map(int, args.blocks.split(",")) for v in map(int, args.variants.split(","))]
-                for blk, var in combos if form and ch == 1 else [(b, 0) for b in map(int, args.dense_blocks.split(","))]:
+                dcombos = [(b, v) for b in map(int, args.dense_blocks.split(",")) for v in map(int, args.variants.split(","))]
+                for blk, var in combos if form and ch == 1 else dcombos:
                     lib.pm_hip_debug_dfa_block(blk)
                     lib.pm_hip_debug_dfa_variant(var)
                     dst = ref if first else out
-                    ms = timed(lambda: m.scan_device(text.data_ptr(), 0, 0, n, dst.data_ptr(), None, s.cuda_stream))
+                    ms = timed(lambda: m.scan_device(text.data_ptr(), 0, 0, n, dst.data_ptr(), None, s.cuda_stream,
+                                                     out_width=args.width))
                     same = True if first else bool(torch.equal(out, ref))
                     first = False
                     key = f"{stream}/{'sparse' if form else 'dense'}/L{lanes}/ch{ch}/b{blk}/v{var}"
