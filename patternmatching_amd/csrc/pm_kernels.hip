@@ -1583,13 +1583,13 @@ constexpr int DFA_CHAINS = 2, SDFA_CHAINS = 1;
 // 10.8 -> 9.7, ASCII 6.82 -> 6.15 at 512 lanes per CU; profiles/r02).
 constexpr int SDFA_BLK = 32;
 static int g_sdfa_blk = SDFA_BLK;
-// The dense coded kernel with u32 ids: 32 positions per block (one whole
-// 128-B line of ids per lane and segment) measured faster at every shape:
-// shipped stream 4.32 -> 3.84 ms, ASCII 6.58 -> 5.93, lines 20.5 -> 19.8 at
-// 512 lanes x 2 segments (profiles/r02/dfa_dense_block_sweep.txt).
+// The dense coded kernel: 32 positions per block (one whole 128-B line of
+// u32 ids per lane and segment) measured faster at every shape: shipped
+// stream 4.32 -> 3.84 ms, ASCII 6.58 -> 5.93, lines 20.5 -> 19.8 at 512
+// lanes x 2 segments (profiles/r02/dfa_dense_block_sweep.txt); with u16 ids
+// 5.23 -> 4.30, 6.40 -> 5.58, 19.8 -> 19.3 (dfa_dense_u16_block_ab.txt).
 constexpr int DFA_DENSE_BLK = 32;
 static int g_dfa_dense_blk = DFA_DENSE_BLK;
-static int g_dfa_dense_blk16 = 16;  // the same for u16 ids (timing experiment: pm_dfa_set_variant 64 -> 32)
 static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64-position blocks)
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
@@ -1609,9 +1609,8 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
     const int64_t align = sparse && (ch == 1 || outw == 4) ? ((g_sdfa_var & 8) ? 64 : g_sdfa_blk)
-                          : !sparse && t.coded && outw == 4 ? g_dfa_dense_blk
-                          : !sparse && t.coded && outw == 2 && ch == 2 ? g_dfa_dense_blk16
-                                                                       : 16;  // whole blocks per segment
+                          : !sparse && t.coded && outw != 0 ? g_dfa_dense_blk
+                                                            : 16;  // whole blocks per segment
     seg = (seg + align - 1) / align * align;
     const int64_t nseg = (n + seg - 1) / seg;
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
@@ -1654,22 +1653,22 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (t.coded) {
 #define DC(W, C) \
     hipLaunchKernelGGL((dfa_coded_kernel<W, C>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, t.out, t.warm, seg)
-        if (g_dfa_dense_blk == 32 && outw == 4) {
-            if (ch == 2)
-                hipLaunchKernelGGL((dfa_coded_kernel<4, 2, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count,
-                                   t.next, t.out, t.warm, seg);
-            else
-                hipLaunchKernelGGL((dfa_coded_kernel<4, 1, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count,
-                                   t.next, t.out, t.warm, seg);
-        } else if (g_dfa_dense_blk16 == 32 && outw == 2 && ch == 2) {  // timing experiment (pm_dfa_set_variant 64)
-            hipLaunchKernelGGL((dfa_coded_kernel<2, 2, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count,
-                               t.next, t.out, t.warm, seg);
+#define DC32(W, C)                                                                                               \
+    hipLaunchKernelGGL((dfa_coded_kernel<W, C, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, \
+                       t.out, t.warm, seg)
+        if (g_dfa_dense_blk == 32 && outw != 0) {
+            if (ch == 2) {
+                if (outw == 4) DC32(4, 2); else DC32(2, 2);
+            } else {
+                if (outw == 4) DC32(4, 1); else DC32(2, 1);
+            }
         } else if (ch == 2) {
             if (outw == 4) DC(4, 2); else if (outw == 2) DC(2, 2); else DC(0, 2);
         } else {
             if (outw == 4) DC(4, 1); else if (outw == 2) DC(2, 1); else DC(0, 1);
         }
 #undef DC
+#undef DC32
         return hipGetLastError();
     }
     if (outw == 4)
@@ -1688,10 +1687,7 @@ void pm_dfa_set_block(int blk) {
     g_sdfa_blk = blk == 16 || blk == 32 ? blk : SDFA_BLK;
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
-void pm_dfa_set_variant(int v) {
-    g_sdfa_var = v & 63;
-    g_dfa_dense_blk16 = (v & 64) ? 32 : 16;
-}
+void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }
