@@ -1137,7 +1137,8 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* _
                 if (!act[k]) continue;
                 uint32_t r[BLK];
 #pragma unroll
-                for (int j = 0; j < BLK; ++j) r[j] = code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                for (int j = 0; j < BLK; ++j)  // count only: an escape code is a nonzero id, no lookup
+                    r[j] = OUTW && code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
                 const int64_t i = lo[k] + BLK * b;
                 if (OUTW == 4) {
                     uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
@@ -1295,7 +1296,8 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* 
                 uint32_t r[BLK];
 #pragma unroll
                 for (int j = 0; j < BLK; ++j)
-                    r[j] = (VAR & 4) || (VAR & 16) ? code[k][j] : code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                    r[j] = (VAR & 4) || (VAR & 16) || !OUTW ? code[k][j]
+                           : code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
                 const int64_t i = lo[k] + BLK * b;
                 if (OUTW == 4) {
                     using v4 = __attribute__((ext_vector_type(4))) unsigned int;
