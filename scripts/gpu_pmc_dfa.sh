@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 for st in ship lines; do
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES"; do
-    i=$((i+1))
+    i=$((i+1)); mkdir -p "$OUT/$st"
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/$st/p$i" -o c -- \
        python3 "$ROOT/bench.py" --stream $st --kernel ac --no-cpu --steps 2 --warmup 0 > "$OUT/$st/p$i.log" 2>&1 || { tail "$OUT/$st/p$i.log"; exit 1; }
   done
