@@ -189,6 +189,25 @@ def test_compiled_image_cache_rejects_a_damaged_filter(tmp_path):
     assert FlatImage(pats, pm.KIND_RT, tmp_path).cache_hit
 
 
+def test_compiled_image_cache_rejects_a_damaged_sparse_record(tmp_path):
+    """A cached DFA image whose sparse form has a record falling back to a
+    state without a row (the kernel would read past the row block) is
+    rebuilt, and so is one whose row word's output code disagrees with sout."""
+    pats = pm.Dictionary(dict_paths("et")).patterns()
+    a = FlatImage(pats, pm.KIND_AC, tmp_path)
+    F = int(a.lib.pm_flat_dfa_sparse_rows(a.h))
+    (f,) = tmp_path.glob(f"pm-{pm.KIND_AC}-*.img")
+    good = f.read_bytes()
+    off = section_offset(good, 11)  # sblock: F rows of 256 words, then 4-word records
+    for word, value in ((F * 256 + 3, F), (5, 0xFFF00000 | 1)):
+        raw = bytearray(good)
+        raw[off + 4 * word:off + 4 * word + 4] = value.to_bytes(4, "little")
+        f.write_bytes(bytes(raw))
+        b = FlatImage(pats, pm.KIND_AC, tmp_path)
+        assert not b.cache_hit and np.array_equal(b.array("sblock"), a.array("sblock"))
+        assert FlatImage(pats, pm.KIND_AC, tmp_path).cache_hit
+
+
 def test_duplicate_pattern_last_id_wins_and_caches(tmp_path):
     """a byte string added twice keeps the id added last, as
     ac_add_pattern does (mpac.c:272 `cur->id = id`); the shadowed gid is a
