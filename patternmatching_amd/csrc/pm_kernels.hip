@@ -487,7 +487,11 @@ __device__ __forceinline__ uint32_t rt_tail(const uint8_t* __restrict__ text, in
     return nwalk;
 }
 
-template <int V, int OUTW>
+// EF: issue the prefetch of chunk c + 2 as soon as chunk c's bytes are in
+// the window registers, ahead of the round and the stores (vmcnt retires in
+// order, so a chunk's wait for its bytes then leaves two chunks of stores in
+// flight instead of one).
+template <int V, int OUTW, bool EF = false>
 __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
                                                              int64_t pos0, int64_t n, void* __restrict__ out,
                                                              unsigned long long* __restrict__ count, RtDev t) {
@@ -805,6 +809,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             x[s].x = __builtin_amdgcn_update_dpp(fix, xr[s], 0x138, 0xf, 0xf, false);  // wave_shr:1
             x[s].y = xr[s];
         }
+        if (EF) fetch(xr, xp, c + 2 * cstep);
         // position j = 4s + b of this lane is pc + 256s + 4*lane + b; its key
         // is the LE u24 ending at byte b of x[s].y (bytes i-2, i-1, i)
 #define RT_RAW(j) ((uint32_t)((((uint64_t)x[(j) >> 2].y << 32) | x[(j) >> 2].x) >> (8 * (2 + ((j) & 3)))))
@@ -937,18 +942,20 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 qn = __builtin_amdgcn_readfirstlane(qn + room);
             }
         }
-        fetch(xr, xp, c + 2 * cstep);
+        if (!EF) fetch(xr, xp, c + 2 * cstep);
     };
     // Enter the loop with the memory-op pattern of the steady state (round,
-    // store, prefetch; round, store, prefetch) so the compiler's vmcnt is the
-    // steady-state one.
+    // store, prefetch; round, store, prefetch -- or with EF prefetch, round,
+    // store) so the compiler's vmcnt is the steady-state one.
     Round r0;
+    if (EF) fetch(xa, pa, ch);
     if (kFilter && kRounds) issue(r0, 0);
     stand_in_store();
-    fetch(xa, pa, ch);
+    if (!EF) fetch(xa, pa, ch);
+    if (EF) fetch(xb, pb, ch + cstep);
     if (kFilter && kRounds) issue(rr, 0);
     stand_in_store();
-    fetch(xb, pb, ch + cstep);
+    if (!EF) fetch(xb, pb, ch + cstep);
     for (;;) {  // wave-uniform
         if (ch >= cend) break;
         chunk(xa, pa, ch);
@@ -1528,7 +1535,18 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         else                                                                                                      \
             hipLaunchKernelGGL((rt_scan_kernel<VV, 0>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
     } while (0)
+#define RT_LAUNCH_EF(VV)                                                                                          \
+    do {                                                                                                          \
+        if (outw == 4)                                                                                            \
+            hipLaunchKernelGGL((rt_scan_kernel<VV, 4, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
+        else if (outw == 2)                                                                                       \
+            hipLaunchKernelGGL((rt_scan_kernel<VV, 2, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
+        else                                                                                                      \
+            hipLaunchKernelGGL((rt_scan_kernel<VV, 0, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
+    } while (0)
     switch (variant) {
+        case 100: RT_LAUNCH_EF(0); break;  // early prefetch (timing experiment)
+        case 102: RT_LAUNCH_EF(2); break;
         case 1: RT_LAUNCH(1); break;
         case 2: RT_LAUNCH(2); break;
         case 3: RT_LAUNCH(3); break;
@@ -1543,6 +1561,7 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         default: RT_LAUNCH(0);
     }
 #undef RT_LAUNCH
+#undef RT_LAUNCH_EF
     return hipGetLastError();
 }
 
