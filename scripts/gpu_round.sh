@@ -45,13 +45,13 @@ import csv, glob, json, sys, statistics
 res = {}
 for f in glob.glob(sys.argv[1] + "/pmc/*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "rt_scan_kernel<0, 4>" in r["Kernel_Name"]:  # the product kernel (bench also runs the floor variant)
+        if "rt_scan_kernel<0, 4" in r["Kernel_Name"]:  # the product kernel (bench also runs the floor variant)
             res.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 out = {k: statistics.median(v) for k, v in res.items()}
 print(json.dumps(out))
 json.dump(out, open(sys.argv[1] + "/pmc_summary.json", "w"), indent=1)
 for f in glob.glob(sys.argv[1] + "/prof/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "rt_scan_kernel<0, 4>" in r["Name"]:
+        if "rt_scan_kernel<0, 4" in r["Name"]:
             print("rocprof", r["Name"][:60], "calls", r["Calls"], "avg_ns", r["AverageNs"])
 PY
