@@ -194,6 +194,11 @@ uint32_t pm_flat_dfa_sparse_rows(void* handle);
 /* name: "t12" "filt" "t3h" "rec" "next" "out" "sblock" "sout" "index_of_gid" "parent" "depth";
  * returns element count */
 size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* elem_size);
+/* read_char's host step (the per-byte path, csrc/pm_hoststep.h) over a
+ * whole text from the stream start: the reverse-trie walk (RT image) or
+ * the DFA step (its sparse form; dense rows when dense_rows != 0 or it has
+ * none).  out_gid: n gids.  Returns 0, or -1 when the RT image does not fit. */
+int pm_flat_host_scan(void* handle, const uint8_t* text, size_t n, uint32_t* out_gid, int dense_rows);
 void pm_flat_free(void* handle);
 
 #ifdef __cplusplus

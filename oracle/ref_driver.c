@@ -25,6 +25,14 @@
  *   stats  DICT...                unique patterns, AC states, max length
  *   parse  DICT                   per accepted line: "line hexbytes"
  *   time   SEED MODE NBYTES DICT... time the reference read_char loop (1 core)
+ *   timefile STREAM DICT...       the same over a stream file (e.g. a lines sample)
+ *   parents OUT DICT...           the patterns tree (PatternsTree.h:90-94): per
+ *                                 pattern in add order, u32 code and u32 code of
+ *                                 its PatternsTreeNode->parent (0 = the root)
+ *   suffix OUT SEED NPAIRS DICT...  is_pattern_suffix (PatternsTree.c:485-494)
+ *                                 on sampled pairs: u32 code(first), code(second),
+ *                                 result; half the firsts are on the second's
+ *                                 parent chain, 1/16 are NULL
  */
 #define _GNU_SOURCE
 #include <stdint.h>
@@ -41,9 +49,16 @@
 
 static size_t n_added = 0;
 static void* ac_obj = NULL;
+static pattern_id_t* added = NULL;  /* ids in add order (the tree's nodes) */
+static size_t added_cap = 0;
 
 static void add_cb(void* obj, char* pat, size_t len, pattern_id_t id) {
     (void)obj;
+    if (n_added == added_cap) {
+        added_cap = added_cap ? 2 * added_cap : 4096;
+        added = (pattern_id_t*)realloc(added, added_cap * sizeof(pattern_id_t));
+    }
+    added[n_added] = id;
     ++n_added;
     mps_table[MPS_AC].add_pattern(ac_obj, pat, len, id);
 }
@@ -63,6 +78,7 @@ static Conf* build(char** dicts, int n) {
 static inline uint32_t code_of(pattern_id_t id) {
     if (id == NULL) return 0;
     PatternsTreeNode* n = (PatternsTreeNode*)id;
+    if (n->parent == NULL) return 0; /* the root: null internal id {-1,-1} (PatternsTree.c:69, 247) */
     return (uint32_t)((n->pattern_id.file_number << 24) | n->pattern_id.line_number);
 }
 
@@ -177,6 +193,61 @@ int main(int argc, char** argv) {
         double dt = now() - t0;
         printf("{\"bytes\": %zu, \"seconds\": %.6f, \"MBps\": %.3f, \"nonnull\": %llu, \"build_s\": %.3f}\n",
                n, dt, n / dt / 1e6, (unsigned long long)nonnull, build_s);
+        return 0;
+    }
+    if (!strcmp(mode, "timefile") && argc >= 4) {
+        size_t n;
+        unsigned char* b = read_file(argv[2], &n);
+        double tb = now();
+        build(argv + 3, argc - 3);
+        double build_s = now() - tb;
+        pattern_id_t (*rc)(void*, char) = mps_table[MPS_AC].read_char;
+        uint64_t nonnull = 0;
+        double t0 = now();
+        for (size_t j = 0; j < n; ++j) nonnull += rc(ac_obj, (char)b[j]) != NULL;
+        double dt = now() - t0;
+        printf("{\"bytes\": %zu, \"seconds\": %.6f, \"MBps\": %.3f, \"nonnull\": %llu, \"build_s\": %.3f}\n",
+               n, dt, n / dt / 1e6, (unsigned long long)nonnull, build_s);
+        return 0;
+    }
+    if (!strcmp(mode, "parents") && argc >= 4) {
+        build(argv + 3, argc - 3);
+        FILE* f = fopen(argv[2], "wb");
+        if (!f) { perror(argv[2]); return 1; }
+        for (size_t k = 0; k < n_added; ++k) {
+            PatternsTreeNode* nd = (PatternsTreeNode*)added[k];
+            uint32_t rec[2] = {code_of(added[k]), code_of(nd->parent)};
+            fwrite(rec, 4, 2, f);
+        }
+        fclose(f);
+        return 0;
+    }
+    if (!strcmp(mode, "suffix") && argc >= 6) {
+        uint64_t seed = strtoull(argv[3], 0, 0);
+        size_t npairs = strtoull(argv[4], 0, 0);
+        build(argv + 5, argc - 5);
+        FILE* f = fopen(argv[2], "wb");
+        if (!f) { perror(argv[2]); return 1; }
+        for (size_t k = 0; k < npairs && n_added; ++k) {
+            uint64_t r = oracle_splitmix64((seed << 32) ^ k);
+            pattern_id_t second = added[r % n_added];
+            pattern_id_t first;
+            if (((r >> 40) & 15) == 0) {
+                first = NULL;
+            } else if ((r >> 44) & 1) { /* a node on second's parent chain, below the root */
+                size_t depth = 0;
+                for (PatternsTreeNode* c = (PatternsTreeNode*)second; c->parent; c = c->parent) ++depth;
+                size_t up = (size_t)((r >> 48) % depth);
+                PatternsTreeNode* c = (PatternsTreeNode*)second;
+                while (up--) c = c->parent;
+                first = c;
+            } else {
+                first = added[(r >> 20) % n_added];
+            }
+            uint32_t rec[3] = {code_of(first), code_of(second), (uint32_t)is_pattern_suffix(first, second)};
+            fwrite(rec, 4, 3, f);
+        }
+        fclose(f);
         return 0;
     }
     fprintf(stderr, "bad arguments\n");

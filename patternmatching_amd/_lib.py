@@ -126,6 +126,7 @@ SIGNATURES = {
     "pm_flat_array": (ctypes.c_size_t, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
                                         ctypes.POINTER(ctypes.c_size_t)]),
     "pm_flat_free": (None, [c_vp]),
+    "pm_flat_host_scan": (ctypes.c_int, [c_vp, c_u8p, ctypes.c_size_t, c_u32p, ctypes.c_int]),
 }
 
 _lib = None

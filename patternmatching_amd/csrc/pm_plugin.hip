@@ -27,6 +27,8 @@
 
 #include "pm_flatten.h"
 #include "pm_hip.h"
+#include "pm_host.h"
+#include "pm_hoststep.h"
 #include "pm_kernels.h"
 #include "pm_streamgen.h"
 
@@ -141,8 +143,10 @@ struct PmHip {
     size_t table_bytes = 0;
     uint32_t* spill = nullptr;  // RT deep-walk scratch of scan_device launches
     int64_t spill_cap = 0;
-    // streaming: the carried history and a two-slot pipeline (scan_host)
-    std::vector<uint8_t> hist;
+    // streaming: the carried history (the last stream bytes, at least
+    // max_len of them) and a two-slot pipeline (scan_host)
+    PmHistRing hist;
+    PmHostStep host;  // read_char's per-byte step over host copies of the images (pm_hoststep.h)
     std::vector<pm_pattern_id_t> id_of_gid;  // [0] = PM_NULL_PATTERN_ID
     PipeSlot slot[2];
     double dev_seconds = 0.0;
@@ -430,14 +434,14 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         const size_t m = std::min(pipe, n - done);
         ensure_slot(o, q, m);
         // context: the last `keep` bytes of (history | buf[0, done))
-        const size_t h = std::min(keep, o->hist.size() + done);
+        const size_t h = std::min(keep, o->hist.avail() + done);
         const size_t ctx = (h + 15) & ~(size_t)15;  // new bytes start 16-aligned
         uint8_t* st = q.h_stage + ctx - h;
         if (done >= h) {
             std::memcpy(st, buf + done - h, h);
         } else {
             const size_t from_hist = h - done;
-            std::memcpy(st, o->hist.data() + o->hist.size() - from_hist, from_hist);
+            o->hist.copy_last(st, from_hist);
             std::memcpy(st + from_hist, buf, done);
         }
         q.staged = m <= PIPE_SMALL_POSITIONS;
@@ -473,15 +477,9 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         PipeSlot& q = (a.busy && (!b.busy || a.off < b.off)) ? a : b;
         if (q.busy) finish(q);
     }
-    // carry the last `keep` bytes of the stream
-    if (keep && n) {
-        if (n >= keep) {
-            o->hist.assign(buf + n - keep, buf + n);
-        } else {
-            o->hist.insert(o->hist.end(), buf, buf + n);
-            if (o->hist.size() > keep) o->hist.erase(o->hist.begin(), o->hist.end() - keep);
-        }
-    }
+    // carry the stream's last bytes; the host DFA step re-derives its state
+    o->hist.append(buf, n);
+    o->host.state_valid = false;
 }
 
 PmHip* as(void* obj) { return static_cast<PmHip*>(obj); }
@@ -560,6 +558,26 @@ void pm_hip_compile(void* obj) {
             o->dfa.sF = im.dfa.sF;
         }
     }
+    // read_char's host step keeps the RT image (rt / auto), or the DFA's
+    // sparse block (dense rows when it has none) for the ac kind
+    o->host = PmHostStep();
+    if (o->kind == KIND_RT || o->kind == KIND_AUTO) {
+        o->host.kind = 1;
+        o->host.rt = std::move(im.rt);
+    } else {
+        o->host.kind = 2;
+        DfaImage& h = o->host.dfa;
+        h.states = im.dfa.states;
+        if (!im.dfa.sblock.empty()) {
+            h.sblock = std::move(im.dfa.sblock);
+            h.sout = std::move(im.dfa.sout);
+            h.sF = im.dfa.sF;
+        } else {
+            h.next = std::move(im.dfa.next);
+            h.out = std::move(im.dfa.out);
+        }
+    }
+    o->hist.init(o->max_len);
     o->d_parent = (const uint32_t*)dalloc_copy(o, im.par.parent.data(), im.par.parent.size() * 4);
     o->d_depth = (const uint32_t*)dalloc_copy(o, im.par.depth.data(), im.par.depth.size() * 4);
     o->parent = std::move(im.par.parent);
@@ -577,23 +595,32 @@ void pm_hip_read_block(void* obj, const char* buf, size_t n, pm_pattern_id_t* ou
     scan_host(as(obj), reinterpret_cast<const uint8_t*>(buf), n, nullptr, out);
 }
 
-// The per-byte entry point of the reference ABI.  It runs the same GPU scan
-// on one byte (correct, but one launch per byte): stream drivers use
-// read_block.
+// The per-byte entry point of the reference ABI (mpac.c:304-319 contract,
+// called per byte by measure.c:292-294).  One byte is far too little work for
+// a launch, so it steps the host copy of the object's own flattened image
+// (pm_hoststep.h): the reverse-trie walk over the carried history (rt /
+// auto), or one transition of the flattened DFA (ac).  The history is the
+// one read_block carries, so the two interleave exactly.
 pm_pattern_id_t pm_hip_read_char(void* obj, char c) {
-    pm_pattern_id_t r;
-    pm_hip_read_block(obj, &c, 1, &r);
-    return r;
+    PmHip* o = as(obj);
+    if (!o->compiled) {
+        std::fprintf(stderr, "pm_hip: read before compile\n");
+        std::exit(EXIT_FAILURE);
+    }
+    return o->id_of_gid[pm_host_step(o->host, o->hist, o->max_len, (uint8_t)c)];
 }
 
+// Device tables + the host copy read_char steps + the object (the
+// reference's total_mem counts the automaton the object holds, mpac.c:328).
 size_t pm_hip_total_mem(void* obj) {
     PmHip* o = as(obj);
-    return sizeof(PmHip) + o->table_bytes;
+    return sizeof(PmHip) + o->table_bytes + o->host.bytes();
 }
 
 void pm_hip_reset(void* obj) {
     PmHip* o = as(obj);
     o->hist.clear();
+    o->host.state_valid = false;
     o->dev_seconds = 0.0;
     // a new stream: the auto kernel choice is measured again, for read_block
     // slots and scan_device launches alike (a spill count still in flight
@@ -881,6 +908,36 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
     if (s == "depth") return ret(h->par.depth);
     *data = nullptr;
     *elem_size = 0;
+    return 0;
+}
+
+// read_char's host step (pm_hoststep.h) over a whole text from the stream
+// start: the RT walk (kind 1), or the DFA step (kind 2; its sparse form, or
+// dense rows when dense_rows is set or it has no sparse form).  CPU tests.
+int pm_flat_host_scan(void* handle, const uint8_t* text, size_t n, uint32_t* out_gid, int dense_rows) {
+    PmFlatHandle* h = static_cast<PmFlatHandle*>(handle);
+    PmHostStep st;
+    uint32_t max_len = 0;
+    if (h->kind == 1) {
+        if (!h->rt.fits) return -1;
+        st.kind = 1;
+        st.rt = h->rt;
+        max_len = 512;  // RtImage::fits bounds patterns below 512 bytes
+    } else {
+        st.kind = 2;
+        st.dfa.states = h->dfa.states;
+        if (!dense_rows && !h->dfa.sblock.empty()) {
+            st.dfa.sblock = h->dfa.sblock;
+            st.dfa.sout = h->dfa.sout;
+            st.dfa.sF = h->dfa.sF;
+        } else {
+            st.dfa.next = h->dfa.next;
+            st.dfa.out = h->dfa.out;
+        }
+    }
+    PmHistRing r;
+    r.init(max_len);
+    for (size_t k = 0; k < n; ++k) out_gid[k] = pm_host_step(st, r, max_len, text[k]);
     return 0;
 }
 

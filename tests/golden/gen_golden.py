@@ -7,7 +7,8 @@ own C sources).  The outputs are data: inputs copied from the reference's
 data directories plus the outputs the reference's own Aho-Corasick path
 (Core/src/mpac.c via mps_table[MPS_AC]) produced for them.
 
-    python tests/golden/gen_golden.py
+    python tests/golden/gen_golden.py          # everything
+    python tests/golden/gen_golden.py tree     # only the patterns-tree fixtures
 """
 import hashlib
 import json
@@ -63,7 +64,38 @@ def sha256(path):
         return hashlib.sha256(f.read()).hexdigest()
 
 
+def gen_tree(manifest):
+    """(6) The reference's patterns tree (PatternsTree.h:90-94): each pattern's
+    PatternsTreeNode->parent as codes (tree_<key>.u32.gz: u32 pairs in add
+    order, 0 = the root), and is_pattern_suffix (PatternsTree.c:485-494) on
+    2048 sampled pairs (suffix_<key>.u32: u32 triples first, second, result)."""
+    import gzip
+    manifest["tree"] = {}
+    for key in DICTS:
+        dp = [os.path.join(DATA, d) for d in DICTS[key]]
+        raw = os.path.join("/tmp", f"tree_{key}.u32")
+        run([DRIVER, "parents", raw] + dp)
+        with open(raw, "rb") as f:
+            blob = f.read()
+        out = os.path.join(HERE, f"tree_{key}.u32.gz")
+        with gzip.GzipFile(out, "wb", mtime=0) as f:
+            f.write(blob)
+        suf = os.path.join(HERE, f"suffix_{key}.u32")
+        run([DRIVER, "suffix", suf, "7", "2048"] + dp)
+        manifest["tree"][key] = {"parents": os.path.basename(out), "parents_sha256": hashlib.sha256(blob).hexdigest(),
+                                 "patterns": len(blob) // 8, "suffix": os.path.basename(suf),
+                                 "suffix_sha256": sha256(suf)}
+
+
 def main():
+    if sys.argv[1:] == ["tree"]:  # only section (6), into the existing manifest
+        path = os.path.join(HERE, "manifest.json")
+        with open(path) as f:
+            manifest = json.load(f)
+        gen_tree(manifest)
+        with open(path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return
     if not os.path.exists(DRIVER):
         sys.exit("build the reference driver first: make -C oracle ref")
     os.makedirs(DATA, exist_ok=True)
@@ -151,6 +183,8 @@ def main():
     with open(out, "rb") as f:
         d = f.read()
     manifest["kmp_kat"] = [i // 4 for i in range(0, len(d), 4) if d[i:i + 4] != b"\0\0\0\0"]
+
+    gen_tree(manifest)
 
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

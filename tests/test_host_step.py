@@ -1,0 +1,74 @@
+"""read_char's per-byte host step (csrc/pm_hoststep.cpp) over the object's
+own flattened images -- the reverse-trie walk (rt / auto kinds) and the
+DFA step in both forms (ac kind) -- reproduces the reference's golden
+vectors and the oracle.  CPU only (pm_flat_host_scan); the GPU suite drives
+the same step through pm_hip_read_char interleaved with read_block."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import patternmatching_amd as pm
+from oracle_lib import DATA, GOLDEN, dict_paths, oracle_for
+from table_emulator import FlatImage, gid_to_code
+
+SHIP = np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8)
+_imgs = {}
+
+
+def image(key, kind):
+    if (key, kind) not in _imgs:
+        d = pm.Dictionary(dict_paths(key))
+        img = FlatImage(d.patterns(), kind)
+        _imgs[(key, kind)] = (img, gid_to_code(img, d))
+    return _imgs[(key, kind)]
+
+
+def host_scan(img, text, dense_rows=0):
+    text = np.ascontiguousarray(text, dtype=np.uint8)
+    out = np.empty(max(len(text), 1), np.uint32)
+    rc = img.lib.pm_flat_host_scan(img.h, text.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(text),
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), dense_rows)
+    assert rc == 0
+    return out[:len(text)]
+
+
+FORMS = [(pm.KIND_RT, 0), (pm.KIND_AC, 0), (pm.KIND_AC, 1)]
+
+
+@pytest.mark.parametrize("key", ["et", "snort", "merged"])
+@pytest.mark.parametrize("kind,dense", FORMS)
+def test_host_step_ship_golden(key, kind, dense):
+    img, tab = image(key, kind)
+    gold = np.fromfile(os.path.join(GOLDEN, f"ship_{key}.u32"), dtype="<u4")
+    assert np.array_equal(tab[host_scan(img, SHIP, dense)], gold)
+
+
+@pytest.mark.parametrize("kind,dense", FORMS)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_host_step_random_vs_oracle(kind, dense, mode):
+    img, tab = image("snort", kind)
+    text = pm.gen_stream(1 << 18, seed=21, mode=mode)
+    o = oracle_for("snort")
+    o.reset()
+    assert np.array_equal(tab[host_scan(img, text, dense)], o.scan_codes(text))
+
+
+def test_host_step_lines_like_input_vs_oracle():
+    """Deep input: dictionary patterns back to back (record walks, chains,
+    wide nodes on the RT side; record states on the DFA side)."""
+    d = pm.Dictionary(dict_paths("merged"))
+    pats = d.patterns()
+    rng = np.random.default_rng(5)
+    parts = []
+    for k in rng.integers(0, len(pats), 6000):
+        parts.append(pats[int(k)])
+        parts.append(b"\n")
+    text = np.frombuffer(b"".join(parts), np.uint8)
+    o = oracle_for("merged")
+    o.reset()
+    exp = o.scan_codes(text)
+    for kind, dense in FORMS:
+        img, tab = image("merged", kind)
+        assert np.array_equal(tab[host_scan(img, text, dense)], exp), (kind, dense)
