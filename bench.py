@@ -6,23 +6,36 @@ A "step" is one scan of the rank's whole stream shard (default 1 GiB of
 seeded synthetic ASCII, generated on the device, resident in HBM before the
 timed region) through the HIP kernel, writing the dense per-position match
 ids (u32; the read_block contract).  Shards are independent streams (one per
-rank, distinct seeds): weak scaling, no data-path collective.  The only
-collective is the RCCL all-reduce of match counts and the max-over-ranks
-time.  --layout split instead cuts ONE logical stream of N x --bytes into
-rank shards (patternmatching_amd.shard.shard_plan: each rank generates its
-shard plus the max_len-1 bytes before it as context), so the all-reduced
-match count is that of the whole stream.
+rank, distinct seeds): weak scaling, no data-path collective.  The
+collectives are RCCL all-reduces of match counts, the per-pattern histogram
+and the max-over-ranks time.  --layout split instead cuts ONE logical
+stream of N x --bytes into rank shards (patternmatching_amd.shard.shard_plan:
+each rank generates its shard plus the max_len-1 bytes before it as
+context), so the all-reduced match count is that of the whole stream.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+With --gpus N > 1 and no launcher (no WORLD_SIZE in the environment) the
+process starts N ranks itself (one child process per GPU, rendezvous on
+127.0.0.1) after running the CPU-baseline leg, before anything touches a
+GPU.  Under a launcher WORLD_SIZE must equal --gpus.
+
+The default run (snort, ascii, dense, rt) adds, after the timed steps, two
+more measurements to the same JSON line: `count_only` (the same stream, the
+RT kernel counting matches, no ids written) and `deep` (the lines stream --
+the dictionary's own patterns back to back -- through the `auto` kind, with
+the reference CPU loop timed on a sample of it).
 
 Prints one JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -33,9 +46,13 @@ DATA = os.path.join(REPO, "tests", "golden", "data")
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 WIDTH = {"dense": 4, "dense16": 2, "count": 0}  # bytes written per stream position
+CAND_NAME = {0: "RT", 1: "RT", 2: "AC dense rows", 3: "AC rows + records"}
+# a reference AC object per CPU-baseline process: snort's table is ~1.06 GB
+# (2072 B per state, mpac.c:43-48), so the process count is also bounded by memory
+REF_PROC_BYTES = 1_300_000_000
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -49,113 +66,263 @@ def parse():
                         "auto: RT or the AC-DFA, picked per launch")
     p.add_argument("--stream", default="ascii", choices=["ascii", "bytes", "ship", "lines"],
                    help="ascii / bytes: seeded synthetic (DESIGN.md §5); ship: the reference's shipped "
-                        "dictionaries_generated.stream tiled to --bytes (adversarial: deep matches)")
+                        "dictionaries_generated.stream tiled to --bytes (adversarial: deep matches); lines: "
+                        "the dictionary's patterns drawn at random, '\\n' after each (deep, no period)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--layout", default="shards", choices=["shards", "split"],
                    help="shards: an independent seeded stream per rank; split: one stream of N x --bytes "
                         "cut into rank shards with max_len-1 bytes of context (ascii / bytes streams)")
     p.add_argument("--cpu-sample", type=int, default=256 << 20, help="bytes of the CPU-baseline sample")
+    p.add_argument("--cpu-cores", type=int, default=0,
+                   help="CPU-baseline processes (0 = the job's host-core share, bounded by memory)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-extra", action="store_true", help="skip the count_only and deep measurements")
     p.add_argument("--score", action="store_true",
                    help="after timing, score the ids against the AC-DFA reliable instance on the device "
                         "(measure.c:174-190) and report FP/FN/partial rates (dense mode)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def host_cores():
-    """Host cores this job may use: the box exposes the whole machine to
-    os.cpu_count() but gives a job a share (OMP_NUM_THREADS there)."""
+# --------------------------------------------------------------------------
+# CPU baseline (rank 0, before any GPU call)
+# --------------------------------------------------------------------------
+
+def host_share():
+    """(nproc, share): the machine's CPUs and this job's share of them (the
+    GPU box sets OMP_NUM_THREADS to the job's share; os.cpu_count() shows
+    the whole machine)."""
     n = os.cpu_count() or 1
     share = os.environ.get("OMP_NUM_THREADS")
-    if share and share.isdigit():
-        n = min(n, int(share))
-    return max(1, min(n, 16))
+    s = min(n, int(share)) if share and share.isdigit() and int(share) > 0 else n
+    return n, max(1, s)
 
 
-def cpu_baseline(args):
+def mem_available():
+    try:
+        with open("/proc/meminfo") as f:
+            for ln in f:
+                if ln.startswith("MemAvailable:"):
+                    return int(ln.split()[1]) * 1024
+    except OSError:
+        pass
+    return 16 << 30
+
+
+def stream_sample(kind, dict_key, nbytes, seed):
+    """The CPU sample's bytes: a seeded ascii / bytes stream or a lines
+    stream of the dictionary (pm_gen_lines_dict; no device)."""
+    import patternmatching_amd as pm
+    if kind == "lines":
+        return pm.Dictionary([os.path.join(DATA, x) for x in DICTS[dict_key]]).gen_lines(nbytes, seed)
+    return pm.gen_stream(nbytes, seed, 0 if kind == "ascii" else 1)
+
+
+def cpu_baseline(args, stream=None, sample_bytes=None, multi=True):
     """The reference's own per-byte AC loop (oracle/_ref/ref_driver, built from
     the reference's sources, mps_table[MPS_AC].read_char per byte): on 1 core
-    over the first cpu_sample bytes of the stream, and on every host core as
-    one process per core, each on its own seeded sample (the
-    aggregate is the sum of the per-process rates).  Without that binary the
-    C port of the loop (oracle/ac_oracle.c) is timed on 1 core.  Test
-    infrastructure, used here only as the measured baseline."""
-    mode = 0 if args.stream == "ascii" else 1
+    over the first sample bytes of the stream, and (multi) on the job's host
+    cores as one process per core, each on its own seeded sample (the
+    aggregate is the sum of the per-process rates).  Beside it the C port of
+    the loop (oracle/ac_oracle.c, same bytes, 1 core), so the baseline
+    survives without the reference binary.  Test infrastructure, used here
+    only as the measured baseline."""
+    import patternmatching_amd as pm  # noqa: F401  (host library only: no device call)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_lib import Oracle
+    stream = stream or args.stream
+    nbytes = sample_bytes or args.cpu_sample
     paths = [os.path.join(DATA, d) for d in DICTS[args.dict]]
     ref = os.path.join(REPO, "oracle", "_ref", "ref_driver")
-    sample = f"first {args.cpu_sample} bytes of the seed-{args.seed} {args.stream} stream, {args.dict}.dict"
-    if os.path.exists(ref):
-        try:
-            r = subprocess.run([ref, "time", str(args.seed), str(mode), str(args.cpu_sample)] + paths,
-                               check=True, capture_output=True, text=True, timeout=600)
-            one = json.loads(r.stdout)
-            single = {"value": round(one["MBps"] / 1000.0, 6), "unit": "GB/s", "cores": 1, "seconds": one["seconds"],
-                      "nonnull": one["nonnull"], "sample": sample}
-            P = host_cores()
-            per = max(1 << 20, args.cpu_sample // 2)
-            procs = [subprocess.Popen([ref, "time", str(args.seed + 1000 + k), str(mode), str(per)] + paths,
-                                      stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
-                     for k in range(P)]
-            outs = [json.loads(p.communicate(timeout=900)[0]) for p in procs]
-            agg = sum(o["MBps"] for o in outs) / 1000.0
-            return {"value": round(agg, 6), "unit": "GB/s", "cores": P, "kind": "reference",
-                    "sample": f"{P} concurrent processes (one per core), each the first {per} bytes of its own "
-                              f"seeded {args.stream} stream (seeds {args.seed + 1000}..), {args.dict}.dict; "
-                              "reference Core/src objects, mps_table[MPS_AC].read_char per byte; value = sum of "
-                              "the per-process rates",
-                    "per_core_min": round(min(o["MBps"] for o in outs) / 1000.0, 6),
-                    "single_core": single}
-        except (subprocess.SubprocessError, OSError, ValueError, KeyError):
-            pass
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import patternmatching_amd as pm
-    from oracle_lib import Oracle
+    nproc, share = host_share()
+    sample = f"first {nbytes} bytes of the seed-{args.seed} {stream} stream, {args.dict}.dict"
+    data = stream_sample(stream, args.dict, nbytes, args.seed)
     o = Oracle(paths)
-    secs, nonnull = o.time_scan(pm.gen_stream(args.cpu_sample, args.seed, mode), threads=1)
-    return {"value": round(args.cpu_sample / secs / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": sample + "; oracle/ac_oracle.c per-byte read_char", "seconds": secs, "nonnull": nonnull}
-
-
-def load_traffic(workload_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one
-    exists for this exact workload (profiles/traffic.json)."""
-    path = os.path.join(REPO, "profiles", "traffic.json")
+    secs, nonnull = o.time_scan(data, threads=1)
+    port = {"value": round(nbytes / secs / 1e9, 6), "unit": "GB/s", "cores": 1, "seconds": round(secs, 4),
+            "nonnull": nonnull, "sample": sample + "; oracle/ac_oracle.c per-byte read_char (the C port)"}
+    del o
+    res = {"value": port["value"], "unit": "GB/s", "cores": 1, "kind": "port", "sample": port["sample"],
+           "nproc": nproc, "share": share, "port": port}
+    if not os.path.exists(ref):
+        return res
     try:
-        with open(path) as f:
-            t = json.load(f).get(workload_key)
-        return t
-    except (OSError, ValueError):
-        return None
+        with tempfile.NamedTemporaryFile(prefix="pm_cpu_", suffix=".stream", dir="/tmp", delete=False) as f:
+            data.tofile(f)
+            path = f.name
+        try:
+            r = subprocess.run([ref, "timefile", path] + paths, check=True, capture_output=True, text=True,
+                               timeout=900)
+        finally:
+            os.unlink(path)
+        one = json.loads(r.stdout)
+        single = {"value": round(one["MBps"] / 1000.0, 6), "unit": "GB/s", "cores": 1, "seconds": one["seconds"],
+                  "nonnull": one["nonnull"], "sample": sample}
+        res.update({"value": single["value"], "cores": 1, "kind": "reference",
+                    "sample": sample + "; reference Core/src objects, mps_table[MPS_AC].read_char per byte",
+                    "single_core": single})
+        if not multi or stream not in ("ascii", "bytes"):
+            return res
+        P = args.cpu_cores or min(share, max(1, mem_available() // REF_PROC_BYTES), 64)
+        per = max(1 << 20, nbytes // 2)
+        mode = 0 if stream == "ascii" else 1
+        procs = [subprocess.Popen([ref, "time", str(args.seed + 1000 + k), str(mode), str(per)] + paths,
+                                  stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+                 for k in range(P)]
+        outs = [json.loads(p.communicate(timeout=900)[0]) for p in procs]
+        agg = sum(o["MBps"] for o in outs) / 1000.0
+        res.update({"value": round(agg, 6), "cores": P,
+                    "sample": f"{P} concurrent processes (one per core of the {share}-core share of "
+                              f"{nproc}), each the first {per} bytes of its own seeded {stream} stream (seeds "
+                              f"{args.seed + 1000}..), {args.dict}.dict; reference Core/src objects, "
+                              "mps_table[MPS_AC].read_char per byte; value = sum of the per-process rates",
+                    "per_core_min": round(min(o["MBps"] for o in outs) / 1000.0, 6)})
+    except (subprocess.SubprocessError, OSError, ValueError, KeyError) as e:
+        res["reference_error"] = repr(e)[:200]
+    return res
 
+
+def cpu_legs(args):
+    """Every CPU baseline of this run: the workload's stream, and for the
+    default run's deep measurement a lines-stream sample."""
+    out = {"main": cpu_baseline(args)}
+    if extras_on(args):
+        out["deep"] = cpu_baseline(args, stream="lines", sample_bytes=min(args.cpu_sample, 64 << 20), multi=False)
+    return out
+
+
+def extras_on(args):
+    return (not args.no_extra and args.stream == "ascii" and args.mode == "dense" and args.kernel == "rt"
+            and args.layout == "shards")
+
+
+# --------------------------------------------------------------------------
+# launcher: --gpus N without torchrun
+# --------------------------------------------------------------------------
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """Start args.gpus ranks (this script, one child process per GPU) with
+    the torch.distributed environment a launcher would set.  The CPU leg runs
+    here first, before any process touches a GPU, and reaches rank 0 through
+    a file.  Returns the exit status (the first failing rank's)."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cpu_path = None
+    if not args.no_cpu:
+        with tempfile.NamedTemporaryFile("w", prefix="pm_bench_cpu_", suffix=".json", dir="/tmp", delete=False) as f:
+            json.dump(cpu_legs(args), f)
+            cpu_path = f.name
+        env["PM_BENCH_CPU_JSON"] = cpu_path
+    port = free_port()
+    procs = []
+    try:
+        for r in range(args.gpus):
+            e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                     LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+        rc = 0
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:  # a rank failed: the others would wait at a collective forever
+                        q.terminate()
+            time.sleep(0.2)
+        return rc
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        if cpu_path:
+            os.unlink(cpu_path)
+
+
+# --------------------------------------------------------------------------
+# one rank
+# --------------------------------------------------------------------------
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    if env_world is not None and world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
-    # CPU leg first, before this process touches the GPU
+    # CPU legs first, before this process touches the GPU (every N)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.stream in ("ascii", "bytes"):
-        cpu = cpu_baseline(args)
+    if rank == 0 and not args.no_cpu:
+        path = os.environ.get("PM_BENCH_CPU_JSON")
+        if path:
+            with open(path) as f:
+                cpu = json.load(f)
+        else:
+            cpu = cpu_legs(args)
 
     import torch
     import torch.distributed as dist
+
+    use_dist = world > 1 or os.environ.get("PM_BENCH_DIST") == "1"
+    backend = os.environ.get("PM_BENCH_BACKEND", "nccl")
+    if os.environ.get("PM_BENCH_REHEARSE") == "1":
+        # launcher / rendezvous rehearsal without a GPU (CPU test suite): gloo,
+        # no device, placeholder timings; never a measurement
+        dist.init_process_group("gloo")
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t)
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid()})
+        if rank == 0:
+            print(json.dumps({"rehearsal": True, "n_gpus": dist.get_world_size(), "world_size": dist.get_world_size(),
+                              "rank_sum": t.item(), "per_rank": ranks, "cpu_baseline": cpu and cpu["main"]}),
+                  flush=True)
+        dist.destroy_process_group()
+        return
+
     import patternmatching_amd as pm
 
     # one GPU per rank; a rehearsal with more ranks than GPUs (gloo) shares them
     dev = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    # the RCCL path runs for world > 1; PM_BENCH_DIST=1 runs it at world 1 too
-    # (one-GPU rehearsal of the multi-GPU code: init, barriers, all-reduces).
-    # PM_BENCH_BACKEND=gloo rehearses several ranks on one GPU.
-    use_dist = world > 1 or os.environ.get("PM_BENCH_DIST") == "1"
-    backend = os.environ.get("PM_BENCH_BACKEND", "nccl")
     if use_dist:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == world
+    coll = "cuda" if backend == "nccl" else "cpu"  # gloo rehearsals reduce host tensors
+
+    def all_reduce(t, op):
+        if not use_dist:
+            return t
+        x = t.to(coll)
+        dist.all_reduce(x, op=op)
+        return x.to(t.device)
+
+    def all_gather(vals):
+        if not use_dist:
+            return [vals]
+        x = torch.tensor(vals, dtype=torch.float64, device=coll)
+        out = [torch.empty_like(x) for _ in range(world)]
+        dist.all_gather(out, x)
+        return [o.tolist() for o in out]
+
     lib = pm.load()
     lib.pm_hip_set_device(dev)
 
@@ -178,61 +345,96 @@ def main():
         ctx_lo = sh.ctx_lo & ~15  # 16-aligned: the scan starts on an aligned position
         pos0, n, gen_off = sh.lo - ctx_lo, sh.hi - sh.lo, ctx_lo
     text = torch.empty(pos0 + n + 64, dtype=torch.uint8, device="cuda")
-    if args.stream == "ship":
-        import numpy as np
-        ship = torch.from_numpy(np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8))
-        reps = (n + 64 + ship.numel() - 1) // ship.numel()
-        text.copy_(ship.to("cuda").repeat(reps)[: n + 64])
-    elif args.stream == "lines":
-        m.gen_lines_device(text.data_ptr(), n + 64, seed, stream.cuda_stream)
-    elif lib.pm_hip_gen_stream_device(text.data_ptr(), gen_off, pos0 + n + 64, seed,
-                                      0 if args.stream == "ascii" else 1, stream.cuda_stream) != 0:
-        raise RuntimeError(lib.pm_hip_last_error().decode())
+
+    def fill(kind, matcher, seed_):
+        if kind == "ship":
+            import numpy as np
+            ship = torch.from_numpy(np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8))
+            reps = (n + 64 + ship.numel() - 1) // ship.numel()
+            text.copy_(ship.to("cuda").repeat(reps)[: n + 64])
+        elif kind == "lines":
+            matcher.gen_lines_device(text.data_ptr(), n + 64, seed_, stream.cuda_stream)
+        elif lib.pm_hip_gen_stream_device(text.data_ptr(), gen_off, pos0 + n + 64, seed_,
+                                          0 if kind == "ascii" else 1, stream.cuda_stream) != 0:
+            raise RuntimeError(lib.pm_hip_last_error().decode())
+
+    fill(args.stream, m, seed)
     width = WIDTH[args.mode]
     out = torch.empty(n, dtype={4: torch.int32, 2: torch.int16}[width], device="cuda") if width else None
     count = torch.zeros(1, dtype=torch.int64, device="cuda")
     out_ptr = out.data_ptr() if out is not None else None
 
-    def step():
-        m.scan_device(text.data_ptr(), 0, pos0, n, out_ptr, count.data_ptr(), stream.cuda_stream, out_width=width or 4)
+    def timed(matcher, steps, warmup, optr, w, cnt):
+        """Pick phase (ac / auto: launches synchronized one by one until the
+        kind holds a choice, at most 12), W warmups, the hold pinned over the
+        timed steps, then `steps` launches between synchronizations and
+        barriers.  Returns (elapsed s, mean kernel ms from hipEvents on the
+        launch stream, held choice)."""
+        def step():
+            matcher.scan_device(text.data_ptr(), 0, pos0, n, optr, cnt.data_ptr(), stream.cuda_stream,
+                                out_width=w or 4)
+        held = matcher.hold_choice(0)
+        for _ in range(12):
+            if held != -1:
+                break
+            step()
+            torch.cuda.synchronize()
+            held = matcher.hold_choice(0)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        held = matcher.hold_choice(steps + 1)
+        if use_dist:
+            dist.barrier()
+        cnt.zero_()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            evs[k][0].record(stream)
+            step()
+            evs[k][1].record(stream)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if use_dist:
+            dist.barrier()
+        return t1 - t0, sum(a.elapsed_time(b) for a, b in evs) / steps, held
 
-    # ac / auto pick their kernel by timing it (an RT launch, then two launches
-    # of each DFA form): let that finish before the W warmups so the timed
-    # steps run the held choice (pm_plugin.hip AUTO_HOLD)
-    pick_launches = {"rt": 0, "ac": 5, "auto": 6}[args.kernel]
-    for _ in range(pick_launches + args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    count.zero_()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        evs[k][0].record(stream)
-        step()
-        evs[k][1].record(stream)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if use_dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    elapsed_mine, kernel_ms_mine, held = timed(m, args.steps, args.warmup, out_ptr, width, count)
+    per_rank = all_gather([float(rank), elapsed_mine, kernel_ms_mine])
+    stats = all_reduce(torch.tensor([elapsed_mine, kernel_ms_mine], dtype=torch.float64, device="cuda"),
+                       dist.ReduceOp.MAX)
+    matches = all_reduce(count.clone(), dist.ReduceOp.SUM)  # RCCL over xGMI: the match-count reduction
 
-    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
-    matches = count.clone()
-    if use_dist:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-        dist.all_reduce(matches, op=dist.ReduceOp.SUM)  # RCCL over xGMI: the match-count reduction
     # after the timed region: all-matches (patterns ending at each position,
-    # i.e. the suffix-chain length of each id) and, with --score, accuracy
-    # against the reliable AC instance, both by pm_hip_score_device
+    # i.e. the suffix-chain length of each id), the per-pattern histogram
+    # (all-reduced: SURVEY §8e) and, with --score, accuracy against the
+    # reliable AC instance, all on the device
     extra = {}
     if width == 4:
         sc = torch.zeros(5, dtype=torch.int64, device="cuda")
         m.score_device(out.data_ptr(), out.data_ptr(), n, sc.data_ptr(), stream.cuda_stream)
         allm = sc.clone()
+        hist = torch.zeros(lib.pm_hip_n_patterns(m.obj) + 1, dtype=torch.int64, device="cuda")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(2):  # the second launch is timed (the first pays first-touch costs)
+            hist.zero_()
+            e0.record(stream)
+            m.pattern_counts_device(out.data_ptr(), n, hist.data_ptr(), stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+        hist_ms = e0.elapsed_time(e1)
+        t_ar = time.perf_counter()
+        hist = all_reduce(hist, dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+        ar_ms = (time.perf_counter() - t_ar) * 1e3
+        extra["pattern_counts"] = {"patterns_seen": int((hist > 0).sum().item()),
+                                   "occurrences_per_step": int(hist.sum().item()),
+                                   "kernel_ms": round(hist_ms, 4),
+                                   "all_reduce_ms": round(ar_ms, 3) if use_dist else None,
+                                   "what": "per-pattern occurrences (suffix chains of the ids) of one step, "
+                                           "pm_hip_pattern_counts_device per rank, then an all-reduce (sum) of "
+                                           f"{hist.numel()} u64 over ranks"}
         if args.score:
             ac = pm.HipMatcher("ac")
             ac.add_dictionary(d)
@@ -240,7 +442,6 @@ def main():
             ref = torch.empty(n, dtype=torch.int32, device="cuda")
             ac.scan_device(text.data_ptr(), 0, pos0, n, ref.data_ptr(), None, stream.cuda_stream)
             sc.zero_()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             m.score_device(out.data_ptr(), ref.data_ptr(), n, sc.data_ptr(), stream.cuda_stream)
             e1.record(stream)
@@ -249,19 +450,8 @@ def main():
             extra["accuracy"] = {"reliable": "AC-DFA (HIP)", "positions": n, "success": c[0],
                                  "false_pos_rate": c[3] / n, "false_neg_rate": c[2] / n, "partial_rate": c[1] / n,
                                  "score_ms": round(e0.elapsed_time(e1), 4)}
-            del ref
-            hist = torch.zeros(lib.pm_hip_n_patterns(m.obj) + 1, dtype=torch.int64, device="cuda")
-            for _ in range(2):  # the second launch is timed (the first pays first-touch costs)
-                hist.zero_()
-                e0.record(stream)
-                m.pattern_counts_device(out.data_ptr(), n, hist.data_ptr(), stream.cuda_stream)
-                e1.record(stream)
-                torch.cuda.synchronize()
-            extra["pattern_counts"] = {"patterns_seen": int((hist > 0).sum().item()),
-                                       "occurrences": int(hist.sum().item()),
-                                       "ms": round(e0.elapsed_time(e1), 4)}
-        if use_dist:
-            dist.all_reduce(allm, op=dist.ReduceOp.SUM)
+            del ref, ac
+        allm = all_reduce(allm, dist.ReduceOp.SUM)
         extra["all_matches_per_step"] = int(allm[4].item())
     elapsed, kernel_ms = stats.tolist()
     total_matches = int(matches.item())
@@ -289,8 +479,48 @@ def main():
                      "what": "rt_scan_kernel variant 2 on this GPU: the same loads and stores, no lookups "
                              "(pm_hip_debug_scan_variant); kernel_over_floor = kernel_ms / floor kernel_ms"}
 
+    # the default run's extra lines: count-only on the same stream, and the
+    # deep lines stream through the auto kind
+    count_only = deep = None
+    if extras_on(args):
+        ksteps = min(args.steps, 10)
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        _, c_ms, _ = timed(m, ksteps, 2, None, 0, cnt)
+        c_ms = all_reduce(torch.tensor([c_ms], dtype=torch.float64, device="cuda"), dist.ReduceOp.MAX).item()
+        c_matches = all_reduce(cnt.clone(), dist.ReduceOp.SUM).item() // ksteps
+        count_only = {"kernel": "reverse-suffix-trie walk, count only (no ids written)", "stream": args.stream,
+                      "steps": ksteps, "kernel_ms": round(c_ms, 4),
+                      "stream_gbps": round(world * n / (c_ms * 1e-3) / 1e9, 2),
+                      "matches_per_step": int(c_matches), "matches_per_sec": round(c_matches / (c_ms * 1e-3), 1),
+                      "roofline": {"bound": "hbm", "achieved": round(n / (c_ms * 1e-3) / 1e9, 2),
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(n / (c_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "algorithmic_bytes_per_launch": n}}
+        del m  # the deep leg's images need the room more than this object
+        ma = pm.HipMatcher("auto")
+        ma.add_dictionary(d)
+        ma.compile()
+        fill("lines", ma, seed)
+        dcnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        dsteps = min(args.steps, 5)
+        _, d_ms, d_held = timed(ma, dsteps, 1, out_ptr, 4, dcnt)
+        d_ms = all_reduce(torch.tensor([d_ms], dtype=torch.float64, device="cuda"), dist.ReduceOp.MAX).item()
+        d_matches = all_reduce(dcnt.clone(), dist.ReduceOp.SUM).item() // dsteps
+        ach = n * 5 / (d_ms * 1e-3) / 1e9
+        deep = {"kernel": "auto kind (RT, or after a deep RT launch the faster AC-DFA form by timed trials)",
+                "picked": CAND_NAME.get(d_held, str(d_held)), "stream": "lines", "mode": "dense",
+                "steps": dsteps, "kernel_ms": round(d_ms, 4),
+                "stream_gbps": round(world * n / (d_ms * 1e-3) / 1e9, 2),
+                "matches_per_step": int(d_matches), "matches_per_sec": round(d_matches / (d_ms * 1e-3), 1),
+                "data": "synthetic deep-match stream: the dictionary's own patterns drawn at random (splitmix64 "
+                        "per 1 KiB block), '\\n' after each, generated in HBM (DESIGN.md §5)",
+                "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": n * 5},
+                "cpu_baseline": cpu.get("deep") if cpu else None}
+        ma.free()
+
     if rank == 0:
-        last_kernel = "RT" if m.kernel_last == 1 else {1: "AC dense rows", 2: "AC rows + records"}.get(m.dfa_form_last, "?")
+        last_kernel = CAND_NAME.get(held, "RT") if held > 0 else "RT" if args.kernel == "rt" else "AC"
         total_bytes = world * args.bytes * args.steps  # every rank scans --bytes positions
         value = total_bytes / elapsed / 1e9
         alg_per_pos = 1 + width  # 1 B read + the id written per position
@@ -298,6 +528,7 @@ def main():
         workload_key = f"{args.dict}-{args.stream}-{n}-{args.mode}-{args.kernel}"
         tr = load_traffic(workload_key)
         traffic = tr["traffic_bytes"] if tr else None
+        rates = [args.bytes * args.steps / r[1] / 1e9 for r in per_rank]
         res = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -324,14 +555,17 @@ def main():
                 "stream_bytes_per_gpu": n,
                 "mode": args.mode,
                 "kernel": ("auto: RT, or after a deep RT launch (spill > 10%%) the fastest of RT and timed trials of "
-                           "both AC-DFA forms (last launch: %s)" % last_kernel if args.kernel == "auto" else
-                           "Aho-Corasick DFA, the faster of its two forms by timed trials (last launch: %s)" % last_kernel
+                           "both AC-DFA forms (held: %s)" % last_kernel if args.kernel == "auto" else
+                           "Aho-Corasick DFA, the faster of its two forms by timed trials (held: %s)" % last_kernel
                            if args.kernel == "ac" else "reverse-suffix-trie walk"),
-                "pick_launches": pick_launches,
                 "parallelism": (f"independent stream shards x{world}" if args.layout == "shards" else
                                 f"one {world * args.bytes} B stream split x{world} (max_len-1 B context per shard)"),
                 "layout": args.layout,
             },
+            "world_size": world,
+            "per_rank": [{"rank": int(r[0]), "gbps": round(g, 3), "kernel_ms": round(r[2], 4)}
+                         for r, g in zip(per_rank, rates)],
+            "rank_spread": round(max(rates) / min(rates), 4),
             "matches_per_sec": round(total_matches / elapsed, 1),
             "matches_per_step": total_matches // max(1, args.steps),
             **({"all_matches_per_sec": round(extra["all_matches_per_step"] * args.steps / elapsed, 1)}
@@ -349,11 +583,24 @@ def main():
                 "algorithmic_bytes_per_launch": n * alg_per_pos,
                 "streaming_floor": floor,
             },
-            "cpu_baseline": cpu,
+            "cpu_baseline": cpu["main"] if cpu else None,
+            **({"count_only": count_only} if count_only else {}),
+            **({"deep": deep} if deep else {}),
         }
         print(json.dumps(res), flush=True)
     if use_dist:
         dist.destroy_process_group()
+
+
+def load_traffic(workload_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one
+    exists for this exact workload (profiles/traffic.json)."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(workload_key)
+    except (OSError, ValueError):
+        return None
 
 
 if __name__ == "__main__":

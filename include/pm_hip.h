@@ -109,6 +109,13 @@ int pm_hip_score_device(void* obj, const uint32_t* d_algo, const uint32_t* d_rea
  * (pm_hip_gid_index maps a gid to its add order), accumulated.  Asynchronous. */
 int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, unsigned long long* d_hist,
                                  void* hip_stream);
+/* ac / auto kinds: keep the kernel picked for pm_hip_scan_device launches
+ * (pm_hip_auto_create) for at least the next `launches` launches, so a timed
+ * region never re-measures.  Returns the held kernel (1 = reverse trie,
+ * 2 = AC dense rows, 3 = AC rows + records), 0 when the object has no choice
+ * to make (rt kind, or a single DFA form), -1 while the pick is still being
+ * measured (launch more, synchronize, and ask again). */
+int pm_hip_hold_choice(void* obj, int launches);
 /* Compiled-image cache: compile() keeps the flattened tables of each
  * dictionary in DIR (pm-<kind>-<hash>.img, keyed by the patterns in add order)
  * and reuses them; without a call here, $PM_IMAGE_CACHE names the directory
@@ -129,6 +136,10 @@ void pm_gen_stream_host(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed
  * without the period of a tiled file.  Device and host give the same bytes. */
 int pm_hip_gen_lines_device(void* obj, uint8_t* d_dst, uint64_t n, uint64_t seed, void* hip_stream);
 void pm_gen_lines_host(void* obj, uint8_t* dst, uint64_t n, uint64_t seed);
+/* The same bytes from a loaded dictionary (its patterns in first-occurrence
+ * order, as pm_dict_feed adds them), without a matcher object or a device. */
+struct PmDict;
+void pm_gen_lines_dict(const struct PmDict* d, uint8_t* dst, uint64_t n, uint64_t seed);
 
 uint32_t pm_hip_n_patterns(void* obj);
 uint32_t pm_hip_max_pattern_len(void* obj);

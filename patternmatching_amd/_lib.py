@@ -97,6 +97,7 @@ SIGNATURES = {
     "pm_gen_stream_host": (None, [c_u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
     "pm_hip_gen_lines_device": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     "pm_gen_lines_host": (None, [c_vp, c_u8p, ctypes.c_uint64, ctypes.c_uint64]),
+    "pm_gen_lines_dict": (None, [PmDictP, c_u8p, ctypes.c_uint64, ctypes.c_uint64]),
     "pm_hip_n_patterns": (ctypes.c_uint32, [c_vp]),
     "pm_hip_max_pattern_len": (ctypes.c_uint32, [c_vp]),
     "pm_hip_gid_index": (ctypes.c_uint32, [c_vp, ctypes.c_uint32]),
@@ -126,6 +127,7 @@ SIGNATURES = {
     "pm_flat_array": (ctypes.c_size_t, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
                                         ctypes.POINTER(ctypes.c_size_t)]),
     "pm_flat_free": (None, [c_vp]),
+    "pm_hip_hold_choice": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "pm_flat_host_scan": (ctypes.c_int, [c_vp, c_u8p, ctypes.c_size_t, c_u32p, ctypes.c_int]),
 }
 

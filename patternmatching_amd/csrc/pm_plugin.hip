@@ -281,61 +281,41 @@ hipError_t launch_cand(PmHip* o, AutoPick& ap, int c, const uint8_t* text, int64
     return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, d, o->num_cu, s);
 }
 
-hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
-                  unsigned long long* count, hipStream_t s, uint32_t* spill, int64_t spill_cap, AutoPick& ap) {
-    RtDev t = o->rt;
-    t.spill = spill;
-    t.spill_cap = spill_cap;
-    if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
-    // one DFA form only (an uncoded automaton), or a form forced for timing
-    if (o->kind == KIND_AC && (!o->dfa.sbase || pm_dfa_forced_form())) {
-        ap.last = KIND_AC;
-        ap.last_form = o->dfa.sbase && pm_dfa_forced_form() && pm_dfa_default_sparse() ? 2 : 1;
-        return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
-    }
-    // KIND_AUTO / KIND_AC (see AUTO_SPILL_FRAC): RT launches are measured
-    // (spill count and time); a deep one (or, for KIND_AC, the end of a
-    // hold) starts timed trials of the DFA forms; the fastest per position
-    // then runs AUTO_HOLD launches.  Results are read only once their events
-    // have completed, so no launch waits.
-    if (!ap.ev) {
-        PM_CHECK(hipMalloc(&ap.d_spill, sizeof(unsigned long long)));
-        PM_CHECK(hipHostMalloc(&ap.h_spill, sizeof(unsigned long long), hipHostMallocDefault));
-        PM_CHECK(hipEventCreateWithFlags(&ap.ev, hipEventDisableTiming));
-        for (int c = 0; c < NCAND; ++c) {
-            PM_CHECK(hipEventCreate(&ap.t0[c]));
-            PM_CHECK(hipEventCreate(&ap.t1[c]));
-        }
-    }
+// The DFA forms to try, in order (dense rows, then rows + records).
+void start_trials(const PmHip* o, AutoPick& ap) {
+    ap.nq = 0;
+    ap.queue[ap.nq++] = CAND_DENSE;
+    if (o->dfa.sbase) ap.queue[ap.nq++] = CAND_SPARSE;
+    ap.qi = 0;
+    ap.trial = 0;
+}
+
+// Fold in whatever measurement has landed (KIND_AUTO / KIND_AC, see
+// AUTO_SPILL_FRAC).
+void resolve_pick(const PmHip* o, AutoPick& ap) {
+    if (!ap.ev) return;
     auto elapsed_ns = [&](int c) {
         float ms = 0.f;
         return hipEventElapsedTime(&ms, ap.t0[c], ap.t1[c]) == hipSuccess && ap.n_of[c] > 0
                    ? ms * 1e6 / (double)ap.n_of[c]
                    : 0.0;
     };
-    auto start_trials = [&]() {
-        ap.nq = 0;
-        ap.queue[ap.nq++] = CAND_DENSE;
-        if (o->dfa.sbase) ap.queue[ap.nq++] = CAND_SPARSE;
-        ap.qi = 0;
-        ap.trial = 0;
-    };
-    // measurements are waited for (not polled): a burst of device-side
-    // launches would otherwise outrun them and never adapt; the wait is one
-    // host-side bubble per measurement, i.e. per AUTO_HOLD + trials + 1
-    // launches, and free in the read_block pipeline, which has synchronized
-    // the slot already
-    if (ap.pending && hipEventSynchronize(ap.ev) == hipSuccess) {
+    if (ap.pending && hipEventQuery(ap.ev) == hipSuccess) {
         ap.pending = false;
         ap.ns[CAND_RT] = elapsed_ns(CAND_RT);
         if ((double)*ap.h_spill > AUTO_SPILL_FRAC * (double)ap.n_of[CAND_RT]) {
-            start_trials();
+            start_trials(o, ap);
         } else {  // shallow: RT holds
             ap.chosen = CAND_RT;
             ap.hold = AUTO_HOLD;
         }
     }
-    if (ap.timing && hipEventSynchronize(ap.t1[ap.queue[ap.nq - 1]]) == hipSuccess) {
+    auto trials_done = [&]() {  // every trial's end event (they may sit on different streams)
+        for (int k = 0; k < ap.nq; ++k)
+            if (hipEventQuery(ap.t1[ap.queue[k]]) != hipSuccess) return false;
+        return true;
+    };
+    if (ap.timing && trials_done()) {
         ap.timing = false;
         int best = o->kind == KIND_AUTO ? CAND_RT : ap.queue[0];
         double best_ns = o->kind == KIND_AUTO ? ap.ns[CAND_RT] : 0.0;
@@ -351,11 +331,51 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
         ap.hold = AUTO_HOLD;
         ap.nq = ap.qi = 0;
     }
+}
+
+hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
+                  unsigned long long* count, hipStream_t s, uint32_t* spill, int64_t spill_cap, AutoPick& ap) {
+    RtDev t = o->rt;
+    t.spill = spill;
+    t.spill_cap = spill_cap;
+    if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
+    // one DFA form only (an uncoded automaton), or a form forced for timing
+    if (o->kind == KIND_AC && (!o->dfa.sbase || pm_dfa_forced_form())) {
+        ap.last = KIND_AC;
+        ap.last_form = o->dfa.sbase && pm_dfa_forced_form() && pm_dfa_default_sparse() ? 2 : 1;
+        return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+    }
+    // KIND_AUTO / KIND_AC (see AUTO_SPILL_FRAC): RT launches are measured
+    // (spill count and time); a deep one (or, for KIND_AC, the end of a
+    // hold) starts timed trials of the DFA forms; the fastest per position
+    // then runs AUTO_HOLD launches.
+    // Measurements are polled, never waited for: scan_device stays an
+    // asynchronous launch on the caller's stream.  Until a measurement has
+    // landed the current choice keeps running (a burst of launches queued
+    // ahead of the device adapts once it catches up; bench.py synchronizes
+    // its untimed pick launches, pm_hip_hold_choice).  The read_block
+    // pipeline has synchronized the slot already, so there it lands at the
+    // next call.  Under stream capture nothing is measured (no events, no
+    // copies): the current choice runs.
+    if (!ap.ev) {
+        if (o->kind == KIND_AC) ap.chosen = o->dfa.sbase ? CAND_SPARSE : CAND_DENSE;  // no RT image
+        PM_CHECK(hipMalloc(&ap.d_spill, sizeof(unsigned long long)));
+        PM_CHECK(hipHostMalloc(&ap.h_spill, sizeof(unsigned long long), hipHostMallocDefault));
+        PM_CHECK(hipEventCreateWithFlags(&ap.ev, hipEventDisableTiming));
+        for (int c = 0; c < NCAND; ++c) {
+            PM_CHECK(hipEventCreate(&ap.t0[c]));
+            PM_CHECK(hipEventCreate(&ap.t1[c]));
+        }
+    }
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+        return launch_cand(o, ap, ap.chosen, text, stream_start, pos0, n, out, outw, count, s, t);
+    resolve_pick(o, ap);
     if (ap.hold > 0) {  // hold the chosen kernel
         --ap.hold;
         return launch_cand(o, ap, ap.chosen, text, stream_start, pos0, n, out, outw, count, s, t);
     }
-    if (o->kind == KIND_AC && !ap.timing && ap.qi >= ap.nq) start_trials();
+    if (o->kind == KIND_AC && !ap.timing && ap.qi >= ap.nq) start_trials(o, ap);
     if (!ap.timing && ap.qi < ap.nq) {  // DFA trials: AUTO_TRIAL launches per form, the last one timed
         const int c = ap.queue[ap.qi];
         if (ap.trial == 0) ap.trial = AUTO_TRIAL;
@@ -367,8 +387,10 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
         if (++ap.qi == ap.nq) ap.timing = e == hipSuccess;
         return e;
     }
-    if (ap.timing)  // (not reached: the wait above resolves it) keep the trials' last form
-        return launch_cand(o, ap, ap.queue[ap.nq - 1], text, stream_start, pos0, n, out, outw, count, s, t);
+    // a measurement still in flight: keep running the current choice
+    if (ap.timing || ap.pending)
+        return launch_cand(o, ap, ap.timing ? ap.queue[ap.nq - 1] : ap.chosen, text, stream_start, pos0, n, out, outw,
+                           count, s, t);
     ap.last = KIND_RT;
     ap.last_form = 0;
     t.spill_total = ap.d_spill;
@@ -745,6 +767,16 @@ int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, un
     return 0;
 }
 
+int pm_hip_hold_choice(void* obj, int launches) {
+    PmHip* o = as(obj);
+    if (o->kind == KIND_RT || (o->kind == KIND_AC && (!o->dfa.sbase || pm_dfa_forced_form()))) return 0;
+    AutoPick& ap = o->pick;
+    resolve_pick(o, ap);
+    if (ap.pending || ap.timing || ap.hold <= 0) return -1;
+    ap.hold = std::max(ap.hold, launches);
+    return 1 + ap.chosen;
+}
+
 void pm_hip_set_image_cache(void* obj, const char* dir) { as(obj)->cache_dir = dir ? dir : ""; }
 
 int pm_hip_image_cache_hit(void* obj) { return as(obj)->cache_hit ? 1 : 0; }
@@ -804,15 +836,25 @@ int pm_hip_gen_lines_device(void* obj, uint8_t* d_dst, uint64_t n, uint64_t seed
         return -2;
     }
     lines_table(o);
-    if (!o->d_lines_pats) {
-        PM_CHECK(hipMalloc(&o->d_lines_pats, o->lines_pats.size()));
-        PM_CHECK(hipMalloc(&o->d_lines_offs, o->lines_offs.size() * sizeof(uint32_t)));
-        PM_CHECK(hipMemcpy(o->d_lines_pats, o->lines_pats.data(), o->lines_pats.size(), hipMemcpyHostToDevice));
-        PM_CHECK(hipMemcpy(o->d_lines_offs, o->lines_offs.data(), o->lines_offs.size() * sizeof(uint32_t),
-                           hipMemcpyHostToDevice));
+    hipError_t e = hipSetDevice(o->device);  // the object's device, like every other entry point
+    if (e == hipSuccess && !o->d_lines_pats) {
+        e = hipMalloc(&o->d_lines_pats, o->lines_pats.size());
+        if (e == hipSuccess) e = hipMalloc(&o->d_lines_offs, o->lines_offs.size() * sizeof(uint32_t));
+        if (e == hipSuccess)
+            e = hipMemcpy(o->d_lines_pats, o->lines_pats.data(), o->lines_pats.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(o->d_lines_offs, o->lines_offs.data(), o->lines_offs.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice);
+        if (e != hipSuccess) {  // leave no half-made tables behind
+            if (o->d_lines_pats) (void)hipFree(o->d_lines_pats);
+            if (o->d_lines_offs) (void)hipFree(o->d_lines_offs);
+            o->d_lines_pats = nullptr;
+            o->d_lines_offs = nullptr;
+        }
     }
-    hipError_t e = pm_launch_gen_lines(d_dst, n, o->d_lines_pats, o->d_lines_offs, (uint32_t)o->pats.size(), seed,
-                                       (hipStream_t)hip_stream);
+    if (e == hipSuccess)
+        e = pm_launch_gen_lines(d_dst, n, o->d_lines_pats, o->d_lines_offs, (uint32_t)o->pats.size(), seed,
+                                (hipStream_t)hip_stream);
     if (e != hipSuccess) {
         std::snprintf(g_err, sizeof(g_err), "gen_lines: %s", hipGetErrorString(e));
         return -3;
@@ -827,6 +869,22 @@ void pm_gen_lines_host(void* obj, uint8_t* dst, uint64_t n, uint64_t seed) {
     for (uint64_t lo = 0, b = 0; lo < n; lo += PM_LINES_BLOCK, ++b)
         pm_lines_block(dst + lo, n - lo < PM_LINES_BLOCK ? n - lo : PM_LINES_BLOCK, b, o->lines_pats.data(),
                        o->lines_offs.data(), (uint32_t)o->pats.size(), seed);
+}
+
+// The lines stream of a dictionary's patterns (first-occurrence order, the
+// order pm_dict_feed gives a matcher), with no matcher object: the CPU
+// baseline's deep-input sample (bench.py), generated before any GPU call.
+void pm_gen_lines_dict(const PmDict* d, uint8_t* dst, uint64_t n, uint64_t seed) {
+    if (!d || d->n == 0) return;
+    std::vector<uint8_t> pats;
+    std::vector<uint32_t> offs(1, 0);
+    for (size_t k = 0; k < d->n; ++k) {
+        pats.insert(pats.end(), d->pats[k].bytes, d->pats[k].bytes + d->pats[k].len);
+        offs.push_back((uint32_t)pats.size());
+    }
+    for (uint64_t lo = 0, b = 0; lo < n; lo += PM_LINES_BLOCK, ++b)
+        pm_lines_block(dst + lo, n - lo < PM_LINES_BLOCK ? n - lo : PM_LINES_BLOCK, b, pats.data(), offs.data(),
+                       (uint32_t)d->n, seed);
 }
 
 void pm_gen_stream_host(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode) {

@@ -89,6 +89,13 @@ class Dictionary:
                 out[i] = (ctypes.addressof(par.contents) - base) // size
         return out
 
+    def gen_lines(self, n, seed) -> np.ndarray:
+        """The lines stream of these patterns (pm_gen_lines_dict; the same
+        bytes as HipMatcher.gen_lines of a matcher fed this dictionary)."""
+        buf = np.empty(n, np.uint8)
+        self.lib.pm_gen_lines_dict(self.ptr, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), n, seed)
+        return buf
+
     def __del__(self):
         ptr = getattr(self, "ptr", None)
         if ptr:
@@ -215,6 +222,12 @@ class HipMatcher:
         rc = self.lib.pm_hip_pattern_counts_device(self.obj, d_ids_ptr, n, d_hist_ptr, stream_ptr)
         if rc != 0:
             raise RuntimeError(self.lib.pm_hip_last_error().decode())
+
+    def hold_choice(self, launches):
+        """pm_hip_hold_choice: keep the picked kernel for `launches` more
+        scan_device launches (1 RT, 2 AC dense rows, 3 AC rows + records;
+        0 = nothing to pick; -1 = still measuring)."""
+        return self.lib.pm_hip_hold_choice(self.obj, launches)
 
     def parent_gid(self, gid):
         return self.lib.pm_hip_parent_gid(self.obj, gid)

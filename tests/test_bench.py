@@ -18,7 +18,7 @@ def _bench_args(**kw):
     sys.path.insert(0, REPO)
     import bench
     a = dict(gpus=1, steps=1, warmup=0, dict="et", bytes=1 << 20, mode="dense", kernel="rt", stream="ascii", seed=1,
-             cpu_sample=1 << 20, no_cpu=False, score=False, layout="shards")
+             cpu_sample=1 << 20, cpu_cores=2, no_cpu=False, no_extra=False, score=False, layout="shards")
     a.update(kw)
     return bench, argparse.Namespace(**a)
 
@@ -30,8 +30,51 @@ def test_cpu_baseline_leg_small_sample():
     cpu = bench.cpu_baseline(args)
     assert cpu["unit"] == "GB/s" and cpu["value"] > 0 and cpu["cores"] >= 1
     assert cpu["kind"] in ("reference", "port")
+    assert cpu["port"]["value"] > 0 and cpu["port"]["cores"] == 1  # the C port's rate, always stated
+    assert cpu["nproc"] >= cpu["share"] >= 1
     if cpu["kind"] == "reference":
-        assert cpu["single_core"]["nonnull"] > 0 and cpu["per_core_min"] > 0
+        assert cpu["single_core"]["nonnull"] == cpu["port"]["nonnull"]  # same bytes, same matches
+        assert cpu["per_core_min"] > 0 and cpu["cores"] == 2
+
+
+def test_cpu_baseline_lines_sample():
+    """The deep leg's sample: a lines stream of the dictionary, generated on
+    the host (no device), timed through the reference loop and the port."""
+    bench, args = _bench_args()
+    cpu = bench.cpu_baseline(args, stream="lines", sample_bytes=1 << 20, multi=False)
+    assert cpu["value"] > 0 and cpu["cores"] == 1 and "lines" in cpu["sample"]
+    if cpu["kind"] == "reference":
+        assert cpu["single_core"]["nonnull"] == cpu["port"]["nonnull"] > 0.9 * (1 << 20)
+
+
+def _rehearse(extra, env=None):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py")] + extra
+    e = dict(os.environ, PM_BENCH_REHEARSE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=e, cwd=REPO)
+
+
+def test_gpus_flag_starts_that_many_ranks_without_a_launcher():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts two ranks itself (the
+    rendezvous + collectives rehearsed on gloo without a GPU); the CPU leg
+    runs first and reaches rank 0's line at N = 2."""
+    r = _rehearse(["--gpus", "2", "--dict", "et", "--cpu-sample", str(1 << 20), "--cpu-cores", "2",
+                   "--no-extra"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["rehearsal"] and d["n_gpus"] == 2 and d["world_size"] == 2
+    assert d["rank_sum"] == 3.0 and sorted(x["rank"] for x in d["per_rank"]) == [0, 1]
+    assert len({x["pid"] for x in d["per_rank"]}) == 2
+    assert d["cpu_baseline"]["value"] > 0
+
+
+def test_world_size_mismatch_is_an_error():
+    r = _rehearse(["--gpus", "4", "--no-cpu"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
 
 
 def _run(extra, env=None):
@@ -104,3 +147,39 @@ def test_bench_split_layout_two_ranks_match_one_stream():
     two = json.loads(lines[0])
     assert two["n_gpus"] == 2 and two["config"]["layout"] == "split"
     assert two["matches_per_step"] == whole["matches_per_step"]
+
+
+@pytest.mark.gpu
+def test_bench_gpus_two_self_launched_sums_two_single_runs():
+    """`bench.py --gpus 2` with no launcher on a one-GPU box (two ranks share
+    it; gloo rehearsal backend): n_gpus 2, per-rank rates, and the reduced
+    count equals single-rank runs of the two shards (seeds 1 and 2)."""
+    one = _run(["--mode", "count", "--no-extra"])
+    two_seed = _run(["--mode", "count", "--no-extra", "--seed", "2"])
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--bytes", str(16 << 20), "--steps", "2",
+           "--warmup", "1", "--no-cpu", "--mode", "count", "--no-extra"]
+    e = dict(os.environ, PM_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        e.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=e, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and len(d["per_rank"]) == 2
+    assert d["matches_per_step"] == one["matches_per_step"] + two_seed["matches_per_step"]
+    assert d["rank_spread"] >= 1.0
+
+
+@pytest.mark.gpu
+def test_bench_default_extras():
+    """The default run's count_only and deep objects (small sizes): the deep
+    lines stream through the auto kind picks a DFA form, count-only counts
+    the same matches as the dense run."""
+    d = _run([])
+    c = d["count_only"]
+    assert c["matches_per_step"] == d["matches_per_step"] and c["roofline"]["frac"] > 0
+    deep = d["deep"]
+    assert deep["stream"] == "lines" and deep["kernel_ms"] > 0 and deep["picked"] in (
+        "RT", "AC dense rows", "AC rows + records")
+    assert deep["matches_per_step"] > 0.5 * (16 << 20)

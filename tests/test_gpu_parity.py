@@ -110,18 +110,35 @@ def test_read_block_pipeline_blocks(kind):
     assert np.array_equal(ids.astype(np.uint64), pid[exp])
 
 
+@pytest.mark.parametrize("key", ["et", "merged"])
 @pytest.mark.parametrize("kind", KINDS)
-def test_read_char_per_byte(kind):
-    m = matcher("merged", kind)
-    o = oracle_for("merged")
-    o.reset()
-    exp = o.scan_codes(SHIP[:160])
-    d = m._dict
-    got = []
-    for c in SHIP[:160].tolist():
-        pid = m.read_char(c)
-        got.append(m.lib.pm_pattern_code(pid))
-    assert got == exp.tolist()
+def test_read_char_per_byte(kind, key):
+    """read_char (the host step over the object's images, pm_hoststep.h)
+    over all 10,240 shipped bytes, interleaved with read_block calls of
+    uneven sizes: the state carries both ways (mps.h:41-42), every position
+    equals the reference's golden vector."""
+    m = matcher(key, kind)
+    gold = np.fromfile(os.path.join(GOLDEN, f"ship_{key}.u32"), dtype="<u4")
+    got = np.zeros(len(SHIP), np.uint32)
+    rng = np.random.default_rng(11)
+    i = 0
+    per_byte = 0
+    while i < len(SHIP):
+        if rng.random() < 0.5:  # a run of read_char calls
+            k = min(len(SHIP) - i, int(rng.integers(1, 700)))
+            for j in range(i, i + k):
+                got[j] = m.lib.pm_pattern_code(m.read_char(int(SHIP[j])))
+            per_byte += k
+        else:  # a read_block of 0..900 bytes
+            k = min(len(SHIP) - i, int(rng.integers(0, 900)))
+            got[i:i + k] = m.read_block_codes(SHIP[i:i + k])
+        i += k
+    assert per_byte > len(SHIP) // 4
+    bad = np.nonzero(got != gold)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+    m.reset()  # and after a reset, per byte from the stream start
+    codes = [m.lib.pm_pattern_code(m.read_char(int(c))) for c in SHIP[:2000].tolist()]
+    assert codes == gold[:2000].tolist()
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -505,13 +522,21 @@ def test_full_size_snort_1gib_kernels_agree():
 @pytest.mark.slow
 def test_full_size_merged_4gib_kernels_agree():
     """BASELINE config 5 size (snort + et merged, 4 GiB: four 1 GiB launches
-    of the RT kernel): the two independent kernels agree at every position."""
+    of the RT kernel, pm_kernels.hip launch_rt_impl): the two independent
+    kernels agree at every position, and oracle windows (each with max_len-1
+    bytes of context) match at the 2^30-position seams between the launches
+    -- where the shipped stream is pasted in, so deep walks cross them --
+    at random offsets and at both ends."""
     torch = _torch()
     rt, ac = matcher("merged", "rt"), matcher("merged", "ac")
     n = 4 << 30
     s = torch.cuda.current_stream().cuda_stream
     dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     pm.load().pm_hip_gen_stream_device(dt.data_ptr(), 0, n + 64, 5, 0, s)
+    ship = torch.from_numpy(np.tile(SHIP, 2)).cuda()
+    seams = [k << 30 for k in (1, 2, 3)]
+    for sm in seams:  # deep matches straddling each launch seam
+        dt[sm - 10000:sm - 10000 + ship.numel()] = ship
     a = torch.empty(n, dtype=torch.int32, device="cuda")
     b = torch.empty(n, dtype=torch.int32, device="cuda")
     ca = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -522,7 +547,20 @@ def test_full_size_merged_4gib_kernels_agree():
     assert torch.equal(a, b)
     assert int(ca.item()) == int(cb.item())
     assert int(ca.item()) > 0.95 * n  # merged: ~99 % of ASCII positions match something
-    del a, b, dt
+    del b
+    o = oracle_for("merged")
+    W = o.max_len - 1
+    rng = np.random.default_rng(1)
+    windows = [sm - 32768 for sm in seams] + rng.integers(W, n - 100000, size=4).tolist() + [0, n - 65536]
+    for off in windows:
+        lo = max(0, off - W)
+        o.reset()
+        seg = dt[lo:off + 65536].cpu().numpy()
+        exp = o.scan_codes(seg)[off - lo:]
+        got = rt._codes[a[off:off + 65536].cpu().numpy().view(np.uint32)]
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (off, bad[:5])
+    del a, dt
     torch.cuda.empty_cache()
 
 

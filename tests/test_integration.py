@@ -1,0 +1,118 @@
+"""The drop-in through the reference's own code (SURVEY
+§8b): the plugin table slot is layout-compatible with Core/src/mps.h, the
+INTEGRATION.md registration stub compiles against the reference's headers,
+and the reference's unmodified program loop -- init_mps, measure_instances_stats
+(read_char per byte, measure.c:292-294; the reliable AC and
+measure_success_rate, :300-303) and write_stats_to_file -- runs the HIP
+plugin exactly (oracle/ref_loop.c, oracle/mphip.c; built here by
+oracle/Makefile from the reference's sources, the binary travels to the GPU
+box with libpm.so)."""
+import csv
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_SRC = "/root/reference/Core/src"
+REF_LOOP = os.path.join(REPO, "oracle", "_ref", "ref_loop")
+DATA = os.path.join(REPO, "tests", "golden", "data")
+needs_ref = pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference sources only in the build container")
+
+
+@needs_ref
+def test_plugin_slot_layout_matches_reference_mps_h():
+    """oracle/abi_check.c: _Static_asserts of every MpsElem member's offset
+    and size against PmMpsElem, pattern_id_t vs pm_pattern_id_t, MpsInstance."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "abicheck"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+@needs_ref
+def test_abi_check_fires_on_a_wrong_layout(tmp_path):
+    """The check is not vacuous: a slot with two members swapped fails it."""
+    src = open(os.path.join(REPO, "oracle", "abi_check.c")).read()
+    hdr = open(os.path.join(REPO, "include", "pm_mps.h")).read()
+    bad = hdr.replace("    void (*compile)(void*);\n    pm_pattern_id_t (*read_char)(void*, char);\n    size_t (*total_mem)(void*);",
+                      "    void (*compile)(void*);\n    size_t (*total_mem)(void*);\n    pm_pattern_id_t (*read_char)(void*, char);")
+    assert bad != hdr
+    (tmp_path / "pm_mps.h").write_text(bad)
+    (tmp_path / "abi_check.c").write_text(src)
+    r = subprocess.run(["gcc", "-fsyntax-only", f"-I{REF_SRC}", f"-I{tmp_path}", str(tmp_path / "abi_check.c")],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "offset of" in r.stderr
+
+
+@needs_ref
+def test_registration_stub_and_reference_loop_build():
+    """mphip.c compiles against the reference's mps.h
+    both ways: the unmodified enum, and with the maintainer's enum edit and
+    read_block member."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "refloop"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert os.path.exists(REF_LOOP)
+    r = subprocess.run(["gcc", "-fsyntax-only", "-w", f"-I{REF_SRC}", f"-I{os.path.join(REPO, 'include')}",
+                        "-DMPS_HIP_RT=3", "-DMPS_HIP_AC=4", "-DMPS_HIP_AUTO=5",
+                        os.path.join(REPO, "oracle", "mphip.c")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def _ref_loop(tmp_path, dict_names, stream_path, bg, lmac=None, timeout=600):
+    out = tmp_path / "results.csv"
+    # write_stats_to_file opens O_WRONLY | O_CREAT with no mode (measure.c:348;
+    # SURVEY App. A 3): create the file first so it stays readable
+    out.write_text("")
+    os.chmod(out, 0o644)
+    env = dict(os.environ, PM_REF_BG=bg)
+    if lmac:
+        env["PM_REF_LMAC"] = lmac
+    args = [REF_LOOP]
+    for d in dict_names:
+        args += ["-d", os.path.join(DATA, d)]
+    args += ["-s", str(stream_path), "-o", str(out)]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env, cwd=tmp_path)
+    assert r.returncode == 0, (r.stdout[-1000:], r.stderr[-2000:])
+    rows = list(csv.reader(open(out)))
+    head = rows[0]
+    return {row[0]: dict(zip(head, row)) for row in rows[1:] if row}
+
+
+@pytest.mark.gpu
+def test_reference_loop_runs_the_hip_plugin_exactly(tmp_path):
+    """C1 (et.dict + the shipped stream) through the reference's own
+    program: the HIP rows of its CSV show zero false-positive, false-negative
+    and partial rates against the reference AC, and non-zero memory."""
+    assert os.path.exists(REF_LOOP), "build it in the build container: make -C oracle refloop"
+    res = _ref_loop(tmp_path, ["et.dict"], os.path.join(DATA, "dictionaries_generated.stream"), "rt", "auto")
+    assert set(res) == {"Aho-Corasick", "HIP Auto (RT / AC per launch)", "HIP Reverse-Trie"}, res.keys()
+    for name, row in res.items():
+        assert float(row["False Positive Rate"]) == 0.0, (name, row)
+        assert float(row["False Negative Rate"]) == 0.0, (name, row)
+        assert float(row["Partial Success Rate"]) == 0.0, (name, row)
+        assert int(row["Total Memory Used"]) > 0
+
+
+@pytest.mark.gpu
+def test_reference_loop_per_byte_rate(tmp_path):
+    """The per-byte read_char rate through the reference's loop (clock()
+    time of measure.c:290-297, 16 MiB of snort ASCII): the HIP kinds' host
+    step against the reference AC in the same run; all exact."""
+    import patternmatching_amd as pm
+    n = 16 << 20
+    stream = tmp_path / "ascii16M.stream"
+    pm.gen_stream(n, seed=5, mode=0).tofile(stream)
+    res = _ref_loop(tmp_path, ["snort.dict"], stream, "rt", "ac", timeout=900)
+    rates = {}
+    for name, row in res.items():
+        assert float(row["False Positive Rate"]) == 0.0 and float(row["False Negative Rate"]) == 0.0, (name, row)
+        assert float(row["Partial Success Rate"]) == 0.0, (name, row)
+        rates[name] = n / max(float(row["Time (in secs)"]), 1e-9) / 1e6
+    ev = os.environ.get("PM_EVIDENCE_DIR")
+    if ev:
+        os.makedirs(ev, exist_ok=True)
+        with open(os.path.join(ev, "ref_loop_per_byte_rate.json"), "w") as f:
+            json.dump({"bytes": n, "stream": "seed-5 ascii", "dict": "snort.dict", "MBps_per_core": rates,
+                       "what": "reference program loop (oracle/ref_loop.c), read_char per byte, clock() time"}, f)
+    assert rates["HIP Reverse-Trie"] >= rates["Aho-Corasick"], rates
