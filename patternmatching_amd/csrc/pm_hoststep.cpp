@@ -33,11 +33,11 @@ inline uint32_t rec_child(const RtImage& im, const uint32_t* R, uint32_t c, uint
 }
 
 // node = record reached after the newest d bytes
-uint32_t rec_walk(const RtImage& im, const PmHistRing& r, uint32_t node, size_t d, size_t avail) {
+uint32_t rec_walk(const RtImage& im, const uint8_t* p, uint32_t node, size_t d, size_t avail) {
     for (;;) {
         const uint32_t* R = &im.rec[(size_t)node * RT_REC_WORDS];
         if (d >= avail) return R[1];
-        if (!rec_child(im, R, r.back(d), node)) return R[1];
+        if (!rec_child(im, R, p[-(ptrdiff_t)d], node)) return R[1];
         ++d;
     }
 }
@@ -53,30 +53,43 @@ bool t3h_find(const RtImage& im, uint32_t key24, const uint32_t*& e) {
 
 }  // namespace
 
-uint32_t pm_rt_host_answer(const RtImage& im, const PmHistRing& r) {
-    const size_t avail = r.avail();
-    if (avail == 0) return 0;
-    const uint32_t c0 = r.back(0);
-    if (avail == 1) return im.t12[RT_T1_BASE + c0];
-    const uint32_t c1 = r.back(1);
+uint32_t pm_rt_host_answer(const RtImage& im, const uint8_t* p, size_t avail) {
+    if (avail < 3) {  // the stream's first bytes
+        if (avail == 0) return 0;
+        const uint32_t c0 = p[0];
+        if (avail == 1) return im.t12[RT_T1_BASE + c0];
+        return im.t12[(c0 << 8) | p[-1]] & 0x7FFFu;
+    }
+    const uint32_t c0 = p[0], c1 = p[-1];
     const uint32_t v = im.t12[(c0 << 8) | c1];
     const uint32_t best2 = v & 0x7FFFu;
-    if (!(v & RT_CONT16) || avail == 2) return best2;
-    const uint32_t key24 = (uint32_t)r.back(2) | (c1 << 8) | (c0 << 16);
+    const uint32_t key24 = (uint32_t)p[-2] | (c1 << 8) | (c0 << 16);
+    // the kernel's stage-1 Bloom filter (16 KiB, no false negatives), read
+    // whether or not the depth-2 node continues: one rarely taken branch
+    // (~2% of random text) instead of an unpredictable one per byte; a
+    // position failing it has no depth-3 node on its walk
+    const uint32_t f = pm_rt_fhash(key24), m1 = pm_rt_filter_mask(f);
+    const uint32_t go = (v >> 15) & (uint32_t)((im.filt[pm_rt_filter_word(f)] & m1) == m1);
+    if (__builtin_expect(!go, 1)) return best2;
+    const uint32_t* f2 = &im.filt[RT_FILTER_WORDS];
+    const uint32_t g3 = pm_rt_p3hash(key24), m3 = pm_rt_filter_mask(g3);
+    const uint32_t key32 = (avail >= 4 ? (uint32_t)p[-3] : 0u) | (key24 << 8);
+    const uint32_t g4 = pm_rt_s4hash(key32), m4 = pm_rt_filter_mask(g4);
+    if ((f2[pm_rt_p3word(g3)] & m3) != m3 && (f2[pm_rt_s4word(g4)] & m4) != m4) return best2;
     const uint32_t* e;
     if (!t3h_find(im, key24, e)) return best2;
     const uint32_t kind = e[0] >> 25;
     if (kind == 0 || avail < 4) return e[1];
     if (kind == 1) {
-        const uint32_t nch = e[2] >> 24, c3 = r.back(3);
+        const uint32_t nch = e[2] >> 24, c3 = p[-3];
         uint32_t k = 0;
         while (k < nch && ((e[2] >> (8 * k)) & 0xFFu) != c3) ++k;
         if (k >= nch) return e[1];
-        if (nch > 1) return rec_walk(im, r, e[3] + k, 4, avail);
+        if (nch > 1) return rec_walk(im, p, e[3] + k, 4, avail);
         if (!(e[3] & RT_CONT32)) return e[3];
-        return rec_walk(im, r, e[3] & ~RT_CONT32, 4, avail);
+        return rec_walk(im, p, e[3] & ~RT_CONT32, 4, avail);
     }
-    return rec_walk(im, r, e[3] & ~RT_CONT32, 3, avail);
+    return rec_walk(im, p, e[3] & ~RT_CONT32, 3, avail);
 }
 
 uint32_t pm_dfa_host_step(const DfaImage& d, uint32_t& s, uint8_t c) {
@@ -106,7 +119,7 @@ uint32_t pm_dfa_host_step(const DfaImage& d, uint32_t& s, uint8_t c) {
 uint32_t pm_host_step(PmHostStep& h, PmHistRing& r, uint32_t max_len, uint8_t c) {
     if (h.kind == 1) {
         r.push(c);
-        return pm_rt_host_answer(h.rt, r);
+        return pm_rt_host_answer(h.rt, r.newest(), r.avail());
     }
     if (h.kind != 2) {
         r.push(c);
@@ -116,7 +129,8 @@ uint32_t pm_host_step(PmHostStep& h, PmHistRing& r, uint32_t max_len, uint8_t c)
         const size_t keep = max_len ? max_len - 1 : 0;
         const size_t w = r.avail() < keep ? r.avail() : keep;
         h.state = 0;
-        for (size_t k = w; k > 0; --k) (void)pm_dfa_host_step(h.dfa, h.state, r.back(k - 1));
+        const uint8_t* p = r.newest();
+        for (size_t k = w; k > 0; --k) (void)pm_dfa_host_step(h.dfa, h.state, p[1 - (ptrdiff_t)k]);
         h.state_valid = true;
     }
     r.push(c);

@@ -21,44 +21,65 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <vector>
 
 #include "pm_flatten.h"
 
-// The last stream bytes (at least max_len of them), newest at seen - 1.
+// The stream's last bytes (at least max_len of them) in one linear buffer:
+// bytes are appended at `pos` and, when it fills, the last K bytes slide to
+// the front (K >= max_len, the walk's reach), so a walk reads text[i - d] as
+// p[-d] from a plain pointer -- as the kernel does -- instead of through
+// ring indices (a ring cost 2x on the per-byte path).
 struct PmHistRing {
     std::vector<uint8_t> b;
-    uint64_t mask = 0;
-    uint64_t seen = 0;  // bytes pushed since the last clear
+    size_t K = 16;    // bytes kept at a slide (power of two >= max_len)
+    size_t pos = 0;   // bytes in b; the newest is b[pos - 1]
+    uint64_t seen = 0;
 
     void init(uint32_t max_len) {
-        size_t r = 16;
-        while (r < (size_t)max_len + 1) r <<= 1;
-        b.assign(r, 0);
-        mask = r - 1;
+        K = 16;
+        while (K < (size_t)max_len) K <<= 1;
+        b.assign(K < 32768 ? 65536 : 2 * K, 0);
+        pos = 0;
         seen = 0;
     }
-    void clear() { seen = 0; }
-    size_t avail() const { return seen < b.size() ? (size_t)seen : b.size(); }
-    void push(uint8_t c) { b[seen++ & mask] = c; }
+    void clear() {
+        pos = 0;
+        seen = 0;
+    }
+    // bytes a walk may look back over, the newest included (>= min(seen, K))
+    size_t avail() const { return pos; }
+    const uint8_t* newest() const { return b.data() + pos - 1; }
+    void slide() {
+        std::memmove(b.data(), b.data() + pos - K, K);
+        pos = K;
+    }
+    void push(uint8_t c) {
+        if (pos == b.size()) slide();
+        b[pos++] = c;
+        ++seen;
+    }
     void append(const uint8_t* p, size_t n) {
-        if (n > b.size()) {
-            seen += n - b.size();
-            p += n - b.size();
-            n = b.size();
+        seen += n;
+        if (n >= K) {
+            std::memcpy(b.data(), p + n - K, K);
+            pos = K;
+            return;
         }
-        for (size_t k = 0; k < n; ++k) push(p[k]);
+        if (pos + n > b.size()) slide();
+        std::memcpy(b.data() + pos, p, n);
+        pos += n;
     }
     // byte d positions before the newest one (d < avail())
-    uint8_t back(size_t d) const { return b[(seen - 1 - d) & mask]; }
+    uint8_t back(size_t d) const { return b[pos - 1 - d]; }
     // the last h bytes (h <= avail()), oldest first
-    void copy_last(uint8_t* dst, size_t h) const {
-        for (size_t k = 0; k < h; ++k) dst[k] = b[(seen - h + k) & mask];
-    }
+    void copy_last(uint8_t* dst, size_t h) const { std::memcpy(dst, b.data() + pos - h, h); }
 };
 
-// gid of the longest pattern ending at the newest byte of r (0 = none).
-uint32_t pm_rt_host_answer(const RtImage& im, const PmHistRing& r);
+// gid of the longest pattern ending at p[0], the stream's newest byte, with
+// avail bytes readable at p[0], p[-1], ... (0 = none).
+uint32_t pm_rt_host_answer(const RtImage& im, const uint8_t* p, size_t avail);
 
 // One DFA transition on byte c from state s (updated); returns the gid of
 // the longest pattern ending at c.  State 0 is the root in both forms.
