@@ -325,6 +325,8 @@ def main():
 
     lib = pm.load()
     lib.pm_hip_set_device(dev)
+    global HBM_PEAK_GBS
+    HBM_PEAK_GBS = lib.pm_hip_hbm_peak_gbs()  # the one constant the CLI's CSV prices against too
 
     d = pm.Dictionary([os.path.join(DATA, x) for x in DICTS[args.dict]])
     m = pm.HipMatcher(args.kernel)

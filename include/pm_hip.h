@@ -157,6 +157,13 @@ int pm_hip_dfa_form_last(void* obj);
 /* Seconds of device time of the scan kernels issued through read_block
  * since the last reset (hipEvent based). */
 double pm_hip_device_seconds(void* obj);
+/* Bytes per position the last read_block's device scans wrote: 2 (u16 gids,
+ * dictionaries of < 65,536 patterns, pattern-id output) or 4; 0 before any. */
+int pm_hip_last_out_width(void* obj);
+/* The HBM roofline every report prices against: MI355X HBM3E peak, GB/s
+ * (MI355X_MICROARCH.md), shared by the CLI's CSV and bench.py. */
+#define PM_HBM_PEAK_GBS 8000.0
+double pm_hip_hbm_peak_gbs(void);
 /* Bytes of flattened tables per kind, for DESIGN/bench reporting. */
 size_t pm_hip_table_bytes(void* obj);
 const char* pm_hip_last_error(void);

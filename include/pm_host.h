@@ -99,6 +99,7 @@ typedef struct {
     uint64_t nonnull;
     size_t total_mem;
     PmSuccessRate sr;
+    int out_width;             /* id bytes per position the device scans wrote (pm_hip_last_out_width) */
 } PmInstanceStats;
 
 /* Returns 0 on success; prints usage and returns nonzero on bad input. */

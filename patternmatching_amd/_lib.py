@@ -127,6 +127,8 @@ SIGNATURES = {
     "pm_flat_array": (ctypes.c_size_t, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
                                         ctypes.POINTER(ctypes.c_size_t)]),
     "pm_flat_free": (None, [c_vp]),
+    "pm_hip_last_out_width": (ctypes.c_int, [c_vp]),
+    "pm_hip_hbm_peak_gbs": (ctypes.c_double, []),
     "pm_hip_hold_choice": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "pm_flat_host_scan": (ctypes.c_int, [c_vp, c_u8p, ctypes.c_size_t, c_u32p, ctypes.c_int]),
 }

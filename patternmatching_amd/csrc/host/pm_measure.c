@@ -237,6 +237,7 @@ int pm_measure_all(PmConf* conf, PmDict* dict, PmInstanceStats* stats) {
             }
             close(fd);
             st->device_seconds += pm_hip_device_seconds(inst[a].obj);
+            st->out_width = pm_hip_last_out_width(inst[a].obj);
         }
         st->total_mem = e->total_mem(inst[a].obj);
         if (conf->verbose) printf("Done\n");
@@ -278,13 +279,17 @@ int pm_write_stats(const PmConf* conf, const PmInstanceStats* stats) {
         if (!(conf->algo_mask & (1 << a))) continue;
         uint64_t sum = s->sr.success + s->sr.false_pos + s->sr.false_neg + s->sr.partial_suc;
         long double den = sum ? (long double)sum : 1.0L;
-        /* roofline: 5 algorithmic bytes per position (1 read + the u32 id
-         * read_block writes) over the device time, against 8 TB/s HBM */
+        /* roofline: the algorithmic bytes per position the device scans
+         * moved (1 read + the id width they wrote: u16 gids for pattern-id
+         * output of dictionaries under 65,536 patterns, else u32) over the
+         * device time, against the HBM peak bench.py uses too */
         const double dev_gbs = s->device_seconds > 0 ? (double)s->bytes / s->device_seconds / 1e9 : 0.0;
+        const double per_pos = 1.0 + (s->out_width ? s->out_width : 4);
         snprintf(buf, sizeof(buf), "\n%s,%.6f,%zu,%.6Lf,%.6Lf,%.6Lf,%.6f,%.3f,%llu,%llu,%.6g,%d", pm_mps_table[a].name,
                  s->wall_seconds, s->total_mem, (long double)s->sr.false_pos / den,
                  (long double)s->sr.false_neg / den, (long double)s->sr.partial_suc / den, s->device_seconds, dev_gbs,
-                 (unsigned long long)s->nonnull, (unsigned long long)s->bytes, dev_gbs * 5.0 / 8000.0, conf->device);
+                 (unsigned long long)s->nonnull, (unsigned long long)s->bytes, dev_gbs * per_pos / PM_HBM_PEAK_GBS,
+                 conf->device);
         put(fd, buf);
     }
     put(fd, "\n");

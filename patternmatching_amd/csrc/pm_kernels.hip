@@ -66,6 +66,9 @@ constexpr int RT_F2_WORDS = 2048;
 constexpr uint32_t RT_QCAP = 64;        // queue ring per wave (power of two, <= 64: one item per lane)
 constexpr uint32_t RT_ROUND = 40;       // a round is issued once this many are queued
 constexpr int RT_CHUNK = 1024;         // positions per wave iteration
+#ifndef RT_SEG_FORM
+#define RT_SEG_FORM 3  // where a full spill region is resolved (rt_scan_kernel)
+#endif
 constexpr uint32_t CONT16 = 0x8000u;
 constexpr uint32_t CONT32 = 0x80000000u;
 constexpr uint32_t T3H_VALID = 1u << 24;
@@ -793,6 +796,54 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     rr.keep = 0;
     uint32_t xa[4], xb[4], pa, pb;
     int64_t ch = cbeg;
+    // Drain the queue and resolve the spill region (the tail): after the
+    // chunk loop, and inside it when the region could not take a chunk's
+    // overflow -- the region is bounded (t.spill_stride items per wave,
+    // pm_rt_spill_items), so deep input resolves it in several segments
+    // while the loop's prefetched chunks stay in flight.  The test sits in
+    // the push's ring-full branch, which random text never enters.
+    const uint32_t scap = (uint32_t)t.spill_stride;
+    auto resolve = [&]() __attribute__((always_inline)) {
+        if (!kFilter) return;
+        if (rr.n) consume(rr);
+        while (qn) {  // wave-uniform; every round advances each item
+            Round rs;
+            issue(rs, qn);
+            consume(rs);
+        }
+        // the auto kind's measure of deep matches: items the ring could not
+        // hold; count-only queues nothing (every candidate goes to the
+        // region), so there it is the positions the tail had to walk
+        if (kRounds && t.spill_total && sn && lane == 0) atomicAdd(t.spill_total, (unsigned long long)sn);
+        // every placeholder and spill store of this wave complete before
+        // its walks patch or read them
+        __builtin_amdgcn_s_waitcnt(0);
+        if (V == 6) {
+            cnt += sn;  // timing only: the chunk loop without the deep walks
+        } else if (V == 3) {
+            for (uint32_t k = lane; k < sn; k += 64) {
+                const uint32_t item = sp[2 * k + 1];
+                const int64_t i = pos0 + (int64_t)(item & RT_POSMASK);
+                const uint32_t v = rt_one(text, s_t, t, i, stream_start);
+                cnt += (uint32_t)(v != 0u) - (item >> 31);
+                if (OUTW) put_id<OUTW>(out, (int64_t)(item & RT_POSMASK), v);
+            }
+        } else if (V == 7) {
+            rt_tail<OUTW, true>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+        } else if (V == 4) {
+            rt_tail<OUTW, false, 8>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+        } else if (V == 5) {
+            rt_tail<OUTW, false, 6>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+        } else {
+            const uint32_t nwalk = rt_tail<OUTW>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
+            if (!kRounds && t.spill_total && nwalk && lane == 0)
+                atomicAdd(t.spill_total, (unsigned long long)nwalk);
+        }
+        // the tail's stores and its reads of the region complete before the
+        // region is refilled
+        __builtin_amdgcn_s_waitcnt(0);
+        sn = 0;
+    };
     // One chunk: depth<=2 answers from LDS, filter, the previous chunk's
     // round consumed and a new one issued, the store, the push of this
     // chunk's candidates, the prefetch two chunks ahead.
@@ -916,7 +967,13 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 // (in rank order) fill the ring, the rest go to the spill
                 // region, walked after the chunk loop, with whether their
                 // placeholder (t12 of the key) is nonzero
-                const uint32_t room = kRounds ? RT_QCAP - qn - rr.keep : 0u;
+                uint32_t room = kRounds ? RT_QCAP - qn - rr.keep : 0u;
+#if RT_SEG_FORM == 3
+                if (__builtin_expect(sn + (total - room) > scap, 0)) {  // the region could overflow: resolve it first
+                    resolve();
+                    room = kRounds ? min(RT_QCAP, total) : 0u;
+                }
+#endif
                 uint32_t rank = base;
                 while (mm) {
                     const uint32_t j = __builtin_ctz(mm);
@@ -956,6 +1013,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     if (kFilter && kRounds) issue(rr, 0);
     stand_in_store();
     if (!EF) fetch(xb, pb, ch + cstep);
+#if RT_SEG_FORM == 3
     for (;;) {  // wave-uniform
         if (ch >= cend) break;
         chunk(xa, pa, ch);
@@ -963,42 +1021,38 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         chunk(xb, pb, ch + cstep);
         ch += 2 * cstep;
     }
-    if (kFilter) {
-        if (rr.n) consume(rr);
-        while (qn) {  // wave-uniform; every round advances each item
-            Round rs;
-            issue(rs, qn);
-            consume(rs);
-        }
-        // the auto kind's measure of deep matches: items the ring could not
-        // hold; count-only queues nothing (every candidate goes to the
-        // region), so there it is the positions the tail had to walk
-        if (kRounds && t.spill_total && sn && lane == 0) atomicAdd(t.spill_total, (unsigned long long)sn);
-        // every placeholder and spill store of this wave complete before
-        // its walks patch or read them
-        __builtin_amdgcn_s_waitcnt(0);
-        if (V == 6) {
-            cnt += sn;  // timing only: the chunk loop without the deep walks
-        } else if (V == 3) {
-            for (uint32_t k = lane; k < sn; k += 64) {
-                const uint32_t item = sp[2 * k + 1];
-                const int64_t i = pos0 + (int64_t)(item & RT_POSMASK);
-                const uint32_t v = rt_one(text, s_t, t, i, stream_start);
-                cnt += (uint32_t)(v != 0u) - (item >> 31);
-                if (OUTW) put_id<OUTW>(out, (int64_t)(item & RT_POSMASK), v);
-            }
-        } else if (V == 7) {
-            rt_tail<OUTW, true>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
-        } else if (V == 4) {
-            rt_tail<OUTW, false, 8>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
-        } else if (V == 5) {
-            rt_tail<OUTW, false, 6>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
-        } else {
-            const uint32_t nwalk = rt_tail<OUTW>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
-            if (!kRounds && t.spill_total && nwalk && lane == 0)
-                atomicAdd(t.spill_total, (unsigned long long)nwalk);
-        }
+    resolve();
+#elif RT_SEG_FORM == 1
+    for (;;) {  // wave-uniform
+        if (ch >= cend) break;
+        chunk(xa, pa, ch);
+        if (ch + cstep >= cend) break;
+        chunk(xb, pb, ch + cstep);
+        ch += 2 * cstep;
+        // (scalar test) the region could overflow within the next two chunks
+        if (__builtin_expect(sn + 2 * RT_CHUNK > scap, 0)) resolve();
     }
+    resolve();
+#else
+    for (bool done = false; !done;) {  // wave-uniform: segments, each ending in resolve()
+        for (;;) {
+            if (ch >= cend) {
+                done = true;
+                break;
+            }
+            chunk(xa, pa, ch);
+            if (ch + cstep >= cend) {
+                done = true;
+                break;
+            }
+            chunk(xb, pb, ch + cstep);
+            ch += 2 * cstep;
+            // (scalar test) the region could overflow within the next two chunks
+            if (__builtin_expect(sn + 2 * RT_CHUNK > scap, 0)) break;
+        }
+        resolve();
+    }
+#endif
     // the (at most two) chunks that touch the stream start or the tail: one
     // position per thread of the last workgroup (a chunk is 1024 positions),
     // so each costs one walk's latency, not sixteen
@@ -1492,9 +1546,21 @@ static int64_t rt_blocks(int64_t n, int num_cu) {
     const int64_t blocks = (nchunks + RT_WAVES - 1) / RT_WAVES;
     return blocks > num_cu ? num_cu : (blocks < 1 ? 1 : blocks);
 }
+// Spill items per wave region: one per position of the wave's main-loop
+// chunks, capped at RT_SPILL_WAVE_CAP (the kernel resolves a full region
+// and goes on, rt_scan_kernel): 128 KiB per wave, 512 MiB for a 1 GiB launch
+// on 256 CUs instead of 8 B per position (8 GiB).  Side by side on the
+// deep streams (1 GiB snort, dense / count, profiles/r03/spill_cap_ab.txt)
+// caps of 16 / 32 / 64 / 128 chunks and the unbounded region measured
+// equal (shipped 11.33-11.37 ms, lines 15.68-15.86 ms; random ASCII equal).
+#ifndef RT_SPILL_CAP_CHUNKS
+#define RT_SPILL_CAP_CHUNKS 16
+#endif
+constexpr int64_t RT_SPILL_WAVE_CAP = RT_SPILL_CAP_CHUNKS * RT_CHUNK;
 static int64_t rt_spill_stride(int64_t n, int64_t blocks) {
     const int64_t nw = blocks * RT_WAVES;
-    return ((n / RT_CHUNK + nw - 1) / nw) * RT_CHUNK;  // a wave's main-loop chunks, one item per position
+    const int64_t natural = ((n / RT_CHUNK + nw - 1) / nw) * RT_CHUNK;
+    return natural < RT_SPILL_WAVE_CAP ? natural : RT_SPILL_WAVE_CAP;
 }
 
 int64_t pm_rt_spill_items(int64_t n, int num_cu) {

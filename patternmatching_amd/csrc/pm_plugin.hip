@@ -157,6 +157,7 @@ struct PmHip {
     uint8_t* d_lines_pats = nullptr;
     uint32_t* d_lines_offs = nullptr;
     int last_kernel = 0;  // KIND_RT / KIND_AC of the last launch
+    int last_out_width = 0;  // bytes per position the last read_block's scans wrote (2 or 4)
     int last_form = 0;    // its DFA form (1 dense rows, 2 sparse; 0 for RT)
 };
 
@@ -209,9 +210,13 @@ void free_slot(PipeSlot& q) {
     q.cap = 0;
 }
 
-// The RT kernel's spill regions (pm_kernels.h): one 8-B item per position
-// of a launch, grown to the largest launch seen (scratch, not part of the
-// automaton's total_mem).
+// The RT kernel's spill regions (pm_kernels.h): 8-B items, one per position
+// of each wave's chunks up to a bound per wave (the kernel resolves a full
+// region and goes on), so a launch of any size needs at most
+// pm_rt_spill_items(INT64_MAX) items: 512 MiB on 256 CUs.  compile()
+// allocates that for scan_device launches, so no launch frees or
+// allocates (hipFree synchronizes the device); read_block slots size theirs
+// to their block.  Scratch, not part of the automaton's total_mem.
 void ensure_spill(PmHip* o, uint32_t*& buf, int64_t& cap, int64_t n) {
     if (o->kind != KIND_RT && o->kind != KIND_AUTO) return;
     const int64_t need = pm_rt_spill_items(n, o->num_cu);
@@ -426,6 +431,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
     const size_t keep = o->max_len ? o->max_len - 1 : 0;
     const size_t pipe = out_gid ? PIPE_GID_POSITIONS : PIPE_ID_POSITIONS;
     const bool narrow = !out_gid && o->gids.index_of_gid.size() <= 65536;  // u16 gids over PCIe
+    o->last_out_width = narrow ? 2 : 4;
     auto finish = [&](PipeSlot& q) {
         PM_CHECK(hipStreamSynchronize(q.stream));
         float ms = 0.f;
@@ -600,6 +606,7 @@ void pm_hip_compile(void* obj) {
         }
     }
     o->hist.init(o->max_len);
+    ensure_spill(o, o->spill, o->spill_cap, INT64_MAX);  // the bound for any scan_device launch
     o->d_parent = (const uint32_t*)dalloc_copy(o, im.par.parent.data(), im.par.parent.size() * 4);
     o->d_depth = (const uint32_t*)dalloc_copy(o, im.par.depth.data(), im.par.depth.size() * 4);
     o->parent = std::move(im.par.parent);
@@ -902,6 +909,8 @@ int pm_hip_kernel_kind(void* obj) { return as(obj)->kind; }
 int pm_hip_kernel_last(void* obj) { return as(obj)->last_kernel; }
 int pm_hip_dfa_form_last(void* obj) { return as(obj)->last_form; }
 double pm_hip_device_seconds(void* obj) { return as(obj)->dev_seconds; }
+int pm_hip_last_out_width(void* obj) { return as(obj)->last_out_width; }
+double pm_hip_hbm_peak_gbs(void) { return PM_HBM_PEAK_GBS; }
 size_t pm_hip_table_bytes(void* obj) { return as(obj)->table_bytes; }
 
 }  // extern "C"

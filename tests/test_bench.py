@@ -37,6 +37,12 @@ def test_cpu_baseline_leg_small_sample():
         assert cpu["per_core_min"] > 0 and cpu["cores"] == 2
 
 
+def test_hbm_peak_is_the_librarys():
+    bench, _ = _bench_args()
+    import patternmatching_amd as pm
+    assert pm.load().pm_hip_hbm_peak_gbs() == bench.HBM_PEAK_GBS == 8000.0
+
+
 def test_cpu_baseline_lines_sample():
     """The deep leg's sample: a lines stream of the dictionary, generated on
     the host (no device), timed through the reference loop and the port."""
