@@ -198,6 +198,11 @@ void pm_hip_debug_dfa_block(int blk);
  * (bit 0 non-temporal id stores, bit 1 non-temporal text loads, bit 2
  * escapes looked up in the step loop, bit 3 64-position blocks; 0 = product). */
 void pm_hip_debug_dfa_variant(int v);
+/* Timing experiments only: the sparse AC-DFA form's kernel: 0 = the plain
+ * kernel, 1 = LDS rows + register record blocks, 2 = record blocks without
+ * LDS rows, 3 / 4 = (1) with two segments per lane; -1 = the product choice
+ * (2 for ids, 0 for count only). */
+void pm_hip_debug_dfa_lds(int v);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

@@ -58,6 +58,8 @@ void pm_dfa_set_sparse(int sparse);
 bool pm_dfa_forced_form();
 void pm_dfa_set_variant(int v);  // timing experiments of the sparse kernel (u32 ids, one chain)
 void pm_dfa_set_block(int blk);  // sparse form, one chain: positions per block (16 or 32)
+// sparse form's kernel (timing): 0 plain, 1 LDS rows + record blocks (default), 2 record blocks only
+void pm_dfa_set_lds(int v);
 bool pm_dfa_default_sparse();  // the form a launch with DfaDev::form 0 runs
 // counts[0..4] += success, partial, false_neg, false_pos, all_matches of algo
 // against real (n u32 gids each, 16-B aligned); parent/depth: PmParents.

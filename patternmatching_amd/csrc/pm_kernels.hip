@@ -1400,6 +1400,176 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* 
     }
 }
 
+// The sparse form with the transition tiles placed by the memory hierarchy
+// (one segment per lane; DFA_LDS_THREADS lanes per workgroup, one
+// workgroup per CU):
+//  * rows: the first KR rows of the block -- the root and the shallowest
+//    states, in the trie's breadth-first order -- are staged once per
+//    workgroup into LDS (KR KiB); a row step or a record's fallback to one
+//    of them is one ds_read_b32 instead of a scattered global load;
+//  * records: a lane loads the aligned block of 4 records (64 B, one
+//    quarter of a 128-B line) holding its state and keeps it in registers;
+//    records are numbered depth-first, so a walk along a pattern's states
+//    steps through the block without another load (on the lines stream
+//    0.61 instead of 1.08 dependent global loads per byte, simulated).
+// Every other step is the plain form's: a 4-B load of a row word, or at a
+// record whose two slots miss the byte the fallback row's word.
+constexpr int DFA_LDS_THREADS = 512;
+constexpr int DFA_LDS_ROWS = 128;  // KiB of LDS: rows [0, 128)
+__device__ __forceinline__ uint4 pick4(const uint4 (&R)[4], uint32_t k) {
+    const uint4 a = (k & 1u) ? R[1] : R[0], b = (k & 1u) ? R[3] : R[2];
+    return (k & 2u) ? b : a;
+}
+
+template <int KR>
+__device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ base, uint32_t F,
+                                                  const uint32_t* __restrict__ s_rows, uint32_t s, uint32_t c,
+                                                  uint32_t& cb, uint4 (&R)[4]) {
+    const bool isrow = s < F;
+    const uint32_t rec = s - F, b = rec >> 2;
+    uint32_t rv = 0;
+    if (isrow) {
+        if (KR && s < (uint32_t)KR) rv = s_rows[s * 256u + c];
+        else rv = *reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
+    } else if (b != cb) {
+        const uint4* p = reinterpret_cast<const uint4*>(base + F * 1024u + b * 64u);
+        R[0] = p[0];
+        R[1] = p[1];
+        R[2] = p[2];
+        R[3] = p[3];
+        cb = b;
+    }
+    if (isrow) return rv;
+    const uint4 q = pick4(R, rec & 3u);
+    const uint32_t key = c | 0x100u;
+    if ((q.x & 0x1FFu) == key) return q.y;
+    if (((q.x >> 16) & 0x1FFu) == key) return q.z;
+    const uint32_t w = q.w;  // the fallback row
+    if (KR && w < (uint32_t)KR) return s_rows[w * 256u + c];
+    return *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
+}
+
+template <int OUTW, int BLK, int KR, int CH = 1>
+__global__ __launch_bounds__(DFA_LDS_THREADS) void dfa_sparse_lds_kernel(
+    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
+    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
+    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 1];
+    if (KR) {
+        const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_rows);
+        for (uint32_t k = threadIdx.x; k < nr * 64u; k += DFA_LDS_THREADS) dst[k] = src[k];
+        __syncthreads();
+    }
+    const int64_t nseg = (n + seg_len - 1) / seg_len;
+    const int64_t lanes = (int64_t)gridDim.x * DFA_LDS_THREADS;
+    uint32_t cnt = 0;
+    uint32_t cb[CH];  // record block cached in R[k]
+    uint4 R[CH][4];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        cb[k] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) R[k][e] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    // CH segments per lane in lock step (sg0 + k * lanes), their loads in flight together
+    for (int64_t sg0 = (int64_t)blockIdx.x * DFA_LDS_THREADS + threadIdx.x; sg0 < nseg; sg0 += CH * lanes) {
+        int64_t lo[CH], hi[CH], wlo[CH];
+        uint32_t s[CH];
+        int64_t wmax = 0;
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int64_t sg = sg0 + k * lanes;
+            lo[k] = sg < nseg ? pos0 + sg * seg_len : pos0 + n;
+            hi[k] = sg < nseg ? (lo[k] + seg_len < pos0 + n ? lo[k] + seg_len : pos0 + n) : pos0 + n;
+            wlo[k] = lo[k] - warm < stream_start ? stream_start : lo[k] - warm;
+            if (sg >= nseg) wlo[k] = lo[k];
+            s[k] = 0;
+            wmax = lo[k] - wlo[k] > wmax ? lo[k] - wlo[k] : wmax;
+        }
+        for (int64_t j = wmax; j > 0; --j) {  // warm-up from the root, right-aligned
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const bool on = lo[k] - j >= wlo[k];
+                const uint32_t v = sdfa_lds_step<KR>(base, F, s_rows, s[k], on ? text[lo[k] - j] : 0u, cb[k], R[k]);
+                s[k] = on ? v & DFA_STATE_MASK : s[k];
+            }
+        }
+        constexpr int NW = BLK / 4;
+        const int64_t nblk = seg_len / BLK;
+        for (int64_t b = 0; b < nblk; ++b) {
+            bool act[CH];
+            bool any = false;
+            uint32_t W[CH][NW];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                act[k] = lo[k] + BLK * b + BLK <= hi[k];
+                any |= act[k];
+#pragma unroll
+                for (int q = 0; q < BLK / 16; ++q) {
+                    const uint4 w = act[k] ? *reinterpret_cast<const uint4*>(text + lo[k] + BLK * b + 16 * q)
+                                           : make_uint4(0u, 0u, 0u, 0u);
+                    W[k][4 * q] = w.x;
+                    W[k][4 * q + 1] = w.y;
+                    W[k][4 * q + 2] = w.z;
+                    W[k][4 * q + 3] = w.w;
+                }
+            }
+            if (!any) break;
+            uint32_t code[CH][BLK], st[CH][BLK];
+#pragma unroll
+            for (int j = 0; j < BLK; ++j) {
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const uint32_t v =
+                        sdfa_lds_step<KR>(base, F, s_rows, s[k], (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb[k], R[k]);
+                    s[k] = act[k] ? v & DFA_STATE_MASK : s[k];
+                    code[k][j] = v >> 20;
+                    st[k][j] = s[k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                if (!act[k]) continue;
+                uint32_t r[BLK];
+                // (count only: an escape code is a nonzero id, no lookup)
+#pragma unroll
+                for (int j = 0; j < BLK; ++j) r[j] = OUTW && code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                const int64_t i = lo[k] + BLK * b;
+                if (OUTW == 4) {
+                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
+#pragma unroll
+                    for (int q = 0; q < BLK / 4; ++q)
+                        o[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+                }
+                if (OUTW == 2) {
+                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + (i - pos0));
+#pragma unroll
+                    for (int q = 0; q < BLK / 8; ++q)
+                        o[q] = make_uint4(r[8 * q] | r[8 * q + 1] << 16, r[8 * q + 2] | r[8 * q + 3] << 16,
+                                          r[8 * q + 4] | r[8 * q + 5] << 16, r[8 * q + 6] | r[8 * q + 7] << 16);
+                }
+#pragma unroll
+                for (int j = 0; j < BLK; ++j) cnt += r[j] != 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {  // the segments' last (< BLK) positions
+            for (int64_t i = lo[k] + BLK * ((hi[k] - lo[k]) / BLK); i < hi[k]; ++i) {
+                s[k] = sdfa_lds_step<KR>(base, F, s_rows, s[k], text[i], cb[k], R[k]) & DFA_STATE_MASK;
+                const uint32_t v = outt[s[k]];
+                if (OUTW) put_id<OUTW>(out, i - pos0, v);
+                cnt += v != 0u;
+            }
+        }
+    }
+    if (count) {
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
+    }
+}
+
 // Accuracy of one id stream against a reference one (Core/src/measure.c:
 // 174-190 with is_pattern_suffix, PatternsTree.c:485-494), one position per
 // lane-element: equal -> success; algo on real's parent chain -> partial;
@@ -1682,6 +1852,22 @@ static int g_sdfa_blk = SDFA_BLK;
 constexpr int DFA_DENSE_BLK = 32;
 static int g_dfa_dense_blk = DFA_DENSE_BLK;
 static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64-position blocks)
+// The sparse form's kernel: 0 = dfa_sparse_kernel, 1 = dfa_sparse_lds_kernel
+// (LDS rows + register record blocks), 2 = the latter without LDS rows,
+// 3 / 4 = (1) with two segments per lane (16 / 32-position blocks); -1 =
+// the product choice: 2 for ids, 0 for count only.  Side by side (snort, 1
+// GiB, ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json):
+//            lines dense / count   shipped dense / count   ASCII dense / count
+//   0         9.64 / 8.05          10.04 / 5.82            6.25 / 4.85
+//   1         9.82 / 8.77           8.69 / 6.05            6.09 / 5.06
+//   2         9.43 / 8.24           8.78 / 5.90            7.06 / 5.83
+//   3 / 4    29.4 / 26.2 ...       18.3 / 16.7 ...         19.8 / 17.4 ...
+// The PMC says why the LDS rows and the record blocks move the lines stream
+// so little: they cut the L2 requests by 45% (TCP_TCC_READ_REQ 1.30 G ->
+// 0.72 G per launch, all of them L2 hits), but the L2 misses -- the table
+// lines that come from the Infinity Cache or HBM, 0.39 G per launch either
+// way -- are what the kernel waits for; two segments per lane double them.
+static int g_sdfa_lds = -1;
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
 // does not name one (-1: not forced; the plugin then times both forms)
@@ -1694,7 +1880,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : sparse ? SDFA_CHAINS : DFA_CHAINS;
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw ? 2 : 0;
+    const bool lds2 = sparse && sdfa_lds >= 3 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
+    const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const int64_t lanes = (int64_t)num_cu * g_dfa_lanes_per_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
@@ -1707,6 +1895,37 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), b(DFA_THREADS);
+    if (sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains) {
+        // one workgroup of DFA_LDS_THREADS lanes per CU, persistent over
+        // the segments (the LDS rows are staged once per workgroup)
+        const int lch = sdfa_lds >= 3 ? 2 : 1;
+        int64_t wg = (nseg + DFA_LDS_THREADS * lch - 1) / (DFA_LDS_THREADS * lch);
+        const int64_t cap = (int64_t)num_cu * g_dfa_lanes_per_cu / DFA_LDS_THREADS;
+        if (wg > cap) wg = cap;
+        if (wg < 1) wg = 1;
+        const dim3 g2((unsigned)wg), b2(DFA_LDS_THREADS);
+#define DL(W, B, K, C)                                                                                               \
+    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, K, C>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
+                       t.sbase, t.sF, t.sout, t.warm, seg)
+        switch (sdfa_lds) {
+            case 2:  // the register record blocks alone (timing)
+                if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
+                break;
+            case 3:  // two segments per lane
+                if (outw == 4) DL(4, 16, DFA_LDS_ROWS, 2); else if (outw == 2) DL(2, 16, DFA_LDS_ROWS, 2);
+                else DL(0, 16, DFA_LDS_ROWS, 2);
+                break;
+            case 4:
+                if (outw == 4) DL(4, 32, DFA_LDS_ROWS, 2); else if (outw == 2) DL(2, 32, DFA_LDS_ROWS, 2);
+                else DL(0, 32, DFA_LDS_ROWS, 2);
+                break;
+            default:
+                if (outw == 4) DL(4, 32, DFA_LDS_ROWS, 1); else if (outw == 2) DL(2, 32, DFA_LDS_ROWS, 1);
+                else DL(0, 32, DFA_LDS_ROWS, 1);
+        }
+#undef DL
+        return hipGetLastError();
+    }
     if (sparse) {
 #define DS(W, C, B)                                                                                           \
     hipLaunchKernelGGL((dfa_sparse_kernel<W, C, B>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.sbase, \
@@ -1779,6 +1998,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 4 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }

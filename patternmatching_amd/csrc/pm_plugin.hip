@@ -581,7 +581,11 @@ void pm_hip_compile(void* obj) {
         o->dfa.warm = o->max_len ? (int64_t)o->max_len - 1 : 0;
         o->dfa.coded = pm_dfa_coded(im.dfa.states) ? 1 : 0;
         if (!im.dfa.sblock.empty()) {
+            // (+64 zero bytes: the LDS kernel reads records in aligned
+            // blocks of four, the last one past the table's end)
+            im.dfa.sblock.resize(im.dfa.sblock.size() + 16, 0u);
             o->dfa.sbase = (const uint8_t*)dalloc_copy(o, im.dfa.sblock.data(), im.dfa.sblock.size() * 4);
+            im.dfa.sblock.resize(im.dfa.sblock.size() - 16);
             o->dfa.sout = (const uint32_t*)dalloc_copy(o, im.dfa.sout.data(), im.dfa.sout.size() * 4);
             o->dfa.sF = im.dfa.sF;
         }
@@ -813,6 +817,7 @@ void pm_hip_debug_dfa_chains(int chains) { pm_dfa_set_chains(chains); }
 void pm_hip_debug_dfa_sparse(int sparse) { pm_dfa_set_sparse(sparse); }
 void pm_hip_debug_dfa_block(int blk) { pm_dfa_set_block(blk); }
 void pm_hip_debug_dfa_variant(int v) { pm_dfa_set_variant(v); }
+void pm_hip_debug_dfa_lds(int v) { pm_dfa_set_lds(v); }
 void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }
 void pm_hip_debug_dfa_min_seg(int min_seg) { pm_dfa_set_min_seg(min_seg); }
 
