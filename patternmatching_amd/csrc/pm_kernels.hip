@@ -502,21 +502,46 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // CU's LDS.  The stage-1 filter sits at address 0, so a filter word's
     // address is the hash bits alone, and t12 at 16 KiB, which fits the
     // ds_read offset field: neither per-position address needs a base add.
-    __shared__ __attribute__((aligned(16)))
-    uint32_t s_lds[RT_FILTER_WORDS + RT_T2_U16 / 2 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP];
+    // Count only (V = 0, OUTW = 0) needs two bits of a depth-2 answer, not
+    // the answer: whether it is nonzero (the position counts, however deep
+    // its walk goes) and whether it is zero with a depth-2 node that has
+    // children (the position is a candidate for the tail).  It keeps them
+    // as one byte per key, t8 = nz | cand << 1 (64 KiB, derived from t12
+    // while staging), at LDS address 0: the 16-bit key (text[i] << 8 |
+    // text[i-1]) is the byte address, one ds_read_u8, no base add or mask.
+    constexpr bool kT8 = V == 0 && OUTW == 0;
+    constexpr int kLdsWords = kT8 ? RT_T2_U16 / 4 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP
+                                  : RT_FILTER_WORDS + RT_T2_U16 / 2 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP;
+    __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsWords];
     uint32_t* const s_f = s_lds;
-    uint16_t* const s_t = reinterpret_cast<uint16_t*>(s_lds + RT_FILTER_WORDS);
-    uint32_t* const s_f2 = s_lds + RT_FILTER_WORDS + RT_T2_U16 / 2;
-    uint32_t(*const s_qkey)[RT_QCAP] =
-        reinterpret_cast<uint32_t(*)[RT_QCAP]>(s_lds + RT_FILTER_WORDS + RT_T2_U16 / 2 + RT_F2_WORDS);
+    const uint8_t* const s_t8 = reinterpret_cast<const uint8_t*>(s_lds);
+    // (count only: rt_one reads the depth-2 answers from global t12)
+    const uint16_t* const s_t = kT8 ? t.t12 : reinterpret_cast<uint16_t*>(s_lds + RT_FILTER_WORDS);
+    uint32_t* const s_f2 = s_lds + (kT8 ? RT_T2_U16 / 4 : RT_FILTER_WORDS + RT_T2_U16 / 2);
+    uint32_t(*const s_qkey)[RT_QCAP] = reinterpret_cast<uint32_t(*)[RT_QCAP]>(s_f2 + RT_F2_WORDS);
     uint32_t(*const s_qpos)[RT_QCAP] = s_qkey + RT_WAVES;
     {
-        const uint4* src = reinterpret_cast<const uint4*>(t.t12);
-        uint4* dst = reinterpret_cast<uint4*>(s_t);
-        for (int k = threadIdx.x; k < RT_T2_U16 * 2 / 16; k += RT_THREADS) dst[k] = src[k];
         const uint4* fsrc = reinterpret_cast<const uint4*>(t.filt);
-        uint4* fdst = reinterpret_cast<uint4*>(s_f);
-        for (int k = threadIdx.x; k < RT_FILTER_WORDS / 4; k += RT_THREADS) fdst[k] = fsrc[k];
+        if (kT8) {
+            const uint2* src = reinterpret_cast<const uint2*>(t.t12);  // 4 keys per thread step
+            for (int k = threadIdx.x; k < RT_T2_U16 / 4; k += RT_THREADS) {
+                const uint2 v = src[k];
+                const uint32_t e[4] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16};
+                uint32_t w = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t nz = (e[q] & 0x7FFFu) != 0u, cand = !nz && (e[q] & CONT16);
+                    w |= (nz | cand << 1) << (8 * q);
+                }
+                s_lds[k] = w;
+            }
+        } else {
+            const uint4* src = reinterpret_cast<const uint4*>(t.t12);
+            uint4* dst = reinterpret_cast<uint4*>(s_lds + RT_FILTER_WORDS);
+            for (int k = threadIdx.x; k < RT_T2_U16 * 2 / 16; k += RT_THREADS) dst[k] = src[k];
+            uint4* fdst = reinterpret_cast<uint4*>(s_f);
+            for (int k = threadIdx.x; k < RT_FILTER_WORDS / 4; k += RT_THREADS) fdst[k] = fsrc[k];
+        }
         uint4* f2dst = reinterpret_cast<uint4*>(s_f2);
         for (int k = threadIdx.x; k < RT_F2_WORDS / 4; k += RT_THREADS) f2dst[k] = fsrc[RT_FILTER_WORDS / 4 + k];
     }
@@ -867,6 +892,16 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
 #define RT_KEY(j) (RT_RAW(j) & 0xFFFFFFu)
         uint32_t res[16];
         uint32_t cm = 0;  // bit j: position j goes past depth 2
+        if (kT8) {
+            // count only: nonzero answers counted on the scalar unit,
+            // zero answers under a node with children queued (cand)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t v = s_t8[(RT_RAW(j) >> 8) & 0xFFFFu];
+                cm |= (v >> 1) << j;
+                scnt += (uint32_t)__popcll(__ballot(v & 1u));
+            }
+        } else {
 #pragma unroll
         for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
         if (kFilter && kStage1) {
@@ -890,8 +925,6 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 cm &= zm;
             }
         }
-#undef RT_KEY
-#undef RT_RAW
         // nonzero placeholders, counted on the scalar unit: one compare per
         // position into a lane mask, then s_bcnt1
 #pragma unroll
@@ -899,6 +932,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             res[j] &= 0x7FFFu;
             scnt += (uint32_t)__popcll(__ballot(res[j] != 0u));
         }
+        }  // !kT8
+#undef RT_KEY
+#undef RT_RAW
         if (kFilter && kRounds) {
             if (rr.n) consume(rr);                // the round issued last chunk
             issue(rr, qn >= RT_ROUND ? qn : 0u);  // items of earlier chunks (stores issued)
