@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-3 measurement session: GPU tests, smoke, the default bench line, the
+# rocprofv3 kernel stats of the default bench (headline kernel, count-only,
+# the deep leg) and the PMC traffic of the headline kernel.
+# Usage: gpu_round3.sh TAG.  Every GPU step has its own time limit; the first
+# failure ends the script.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd); TAG=${1:-r03}; OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
+export PM_EVIDENCE_DIR=$OUT
+echo "== $(date) host cpus $(nproc) share ${OMP_NUM_THREADS:-?}"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+rc=$?; tail -2 "$OUT/pytest_gpu.log"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1 || { tail "$OUT/smoke.log"; exit 1; }
+tail -1 "$OUT/smoke.log"
+timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail "$OUT/bench.err"; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/bench.json')); print('C3', d['value'], 'kernel_ms', d['kernel_ms'], 'frac', d['roofline']['frac'], 'count', d['count_only']['kernel_ms'], 'deep', d['deep']['kernel_ms'], d['deep']['picked'], 'cpu', d['cpu_baseline']['value'], d['cpu_baseline']['cores'])"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
+    python3 "$ROOT/bench.py" --no-cpu --steps 10 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail "$OUT/bench_prof.err"; exit 1; }
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d "$OUT/pmc/$c" -o c -- \
+    python3 "$ROOT/bench.py" --no-cpu --no-extra --steps 3 --warmup 1 > "$OUT/pmc_$c.log" 2>&1 || { tail "$OUT/pmc_$c.log"; exit 1; }
+done
+python3 - "$OUT" <<'PY'
+import csv, glob, sys, statistics, json
+res = {}
+for f in glob.glob(sys.argv[1] + "/pmc/*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "rt_scan_kernel<0, 4" in r["Kernel_Name"]:
+            res.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+out = {k: statistics.median(v) for k, v in res.items()}
+json.dump(out, open(sys.argv[1] + "/pmc_summary.json", "w"), indent=1)
+print("pmc", out)
+for f in glob.glob(sys.argv[1] + "/prof/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        print("rocprof", r["Name"][:70], "calls", r["Calls"], "avg_ns", r["AverageNs"])
+PY
