@@ -824,6 +824,74 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     assert len(set(zip(kernels[5:], forms[5:]))) == 1, (kernels, forms)
 
 
+def test_auto_scan_device_across_two_streams_and_hold():
+    """The auto kind's pick is polled, never waited for (pm_plugin.hip
+    launch): launches alternating between two streams with no host
+    synchronization are all exact; once they have landed the pick resolves
+    and pm_hip_hold_choice pins it."""
+    import torch
+    n = 8 << 20
+    text = _tiled_ship(n)
+    dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    ref = matcher("et", "ac")
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    m = matcher("et", "auto")
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(12)]
+    for k, o in enumerate(outs):
+        m.scan_device(dt.data_ptr(), 0, 0, n, o.data_ptr(), None, streams[k & 1].cuda_stream)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, want)
+    held = m.hold_choice(0)
+    for _ in range(12):
+        if held > 0:
+            break
+        o = outs[0]
+        m.scan_device(dt.data_ptr(), 0, 0, n, o.data_ptr(), None, streams[0].cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(o, want)
+        held = m.hold_choice(0)
+    assert held in (1, 2, 3), held
+    assert m.hold_choice(100) == held  # pinned for the next 100 launches
+    for _ in range(3):
+        m.scan_device(dt.data_ptr(), 0, 0, n, outs[1].data_ptr(), None, streams[1].cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[1], want)
+        assert m.hold_choice(0) == held
+    assert matcher("et", "rt").hold_choice(5) == 0  # the rt kind has nothing to pick
+
+
+def test_auto_scan_device_under_graph_capture():
+    """scan_device of the auto kind inside a HIP graph capture (torch CUDA
+    graph): nothing is measured under capture (no events, no copies), the
+    current choice is captured, and a replay gives the eager ids."""
+    import torch
+    n = 4 << 20
+    text = _tiled_ship(n)
+    dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    m = matcher("et", "auto")
+    s = torch.cuda.Stream()
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    got = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    with torch.cuda.stream(s):
+        m.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), cnt.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        cnt.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(got, want)
+        assert int(cnt.item()) == int((want != 0).sum().item())
+
+
 @pytest.mark.parametrize("stream", ["ship", "lines"])
 def test_ac_kind_times_both_dfa_forms(stream):
     """The AC kind tries its two forms (two launches each, the second timed)
