@@ -893,14 +893,18 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         uint32_t res[16];
         uint32_t cm = 0;  // bit j: position j goes past depth 2
         if (kT8) {
-            // count only: nonzero answers counted on the scalar unit,
-            // zero answers under a node with children queued (cand)
+            // count only: zero answers under a node with children are queued
+            // (cand, bit 1); the nonzero ones (bit 0) are counted per lane
+            // from the sum of the 16 classes (sum = nz + 2 cand): one add per
+            // position instead of a compare, a ballot and two scalar ops
+            uint32_t sum = 0;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const uint32_t v = s_t8[(RT_RAW(j) >> 8) & 0xFFFFu];
                 cm |= (v >> 1) << j;
-                scnt += (uint32_t)__popcll(__ballot(v & 1u));
+                sum += v;
             }
+            cnt += sum - 2u * (uint32_t)__popc(cm);
         } else {
 #pragma unroll
         for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
