@@ -930,7 +930,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             }
         }
         // nonzero placeholders, counted on the scalar unit: one compare per
-        // position into a lane mask, then s_bcnt1
+        // position into a lane mask, then s_bcnt1 (a per-lane sum, as count
+        // only does, measured equal here: ids, 1.12-1.17 ms either way)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             res[j] &= 0x7FFFu;
