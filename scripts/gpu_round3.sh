@@ -16,8 +16,13 @@ tail -1 "$OUT/smoke.log"
 timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail "$OUT/bench.err"; exit 1; }
 python3 -c "import json; d=json.load(open('$OUT/bench.json')); print('C3', d['value'], 'kernel_ms', d['kernel_ms'], 'frac', d['roofline']['frac'], 'count', d['count_only']['kernel_ms'], 'deep', d['deep']['kernel_ms'], d['deep']['picked'], 'cpu', d['cpu_baseline']['value'], d['cpu_baseline']['cores'])"
 cd /tmp && export TMPDIR=/tmp
+# kernel stats per leg, each its own run so a kernel's average is that leg's
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-    python3 "$ROOT/bench.py" --no-cpu --steps 10 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail "$OUT/bench_prof.err"; exit 1; }
+    python3 "$ROOT/bench.py" --no-cpu --no-extra --steps 10 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail "$OUT/bench_prof.err"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_count" -o bench -- \
+    python3 "$ROOT/bench.py" --no-cpu --no-extra --mode count --steps 10 > "$OUT/bench_prof_count.json" 2> "$OUT/bench_prof_count.err" || { tail "$OUT/bench_prof_count.err"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_deep" -o bench -- \
+    python3 "$ROOT/bench.py" --no-cpu --no-extra --stream lines --kernel auto --steps 5 > "$OUT/bench_prof_deep.json" 2> "$OUT/bench_prof_deep.err" || { tail "$OUT/bench_prof_deep.err"; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d "$OUT/pmc/$c" -o c -- \
     python3 "$ROOT/bench.py" --no-cpu --no-extra --steps 3 --warmup 1 > "$OUT/pmc_$c.log" 2>&1 || { tail "$OUT/pmc_$c.log"; exit 1; }
@@ -32,7 +37,9 @@ for f in glob.glob(sys.argv[1] + "/pmc/*/**/*counter_collection.csv", recursive=
 out = {k: statistics.median(v) for k, v in res.items()}
 json.dump(out, open(sys.argv[1] + "/pmc_summary.json", "w"), indent=1)
 print("pmc", out)
-for f in glob.glob(sys.argv[1] + "/prof/**/*kernel_stats.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        print("rocprof", r["Name"][:70], "calls", r["Calls"], "avg_ns", r["AverageNs"])
+for leg in ("prof", "prof_count", "prof_deep"):
+    for f in glob.glob(sys.argv[1] + f"/{leg}/**/*kernel_stats.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "rt_scan" in r["Name"] or "dfa_" in r["Name"]:
+                print(leg, r["Name"][:60], "calls", r["Calls"], "avg_ns", r["AverageNs"])
 PY
