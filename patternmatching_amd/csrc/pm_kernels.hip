@@ -66,9 +66,6 @@ constexpr int RT_F2_WORDS = 2048;
 constexpr uint32_t RT_QCAP = 64;        // queue ring per wave (power of two, <= 64: one item per lane)
 constexpr uint32_t RT_ROUND = 40;       // a round is issued once this many are queued
 constexpr int RT_CHUNK = 1024;         // positions per wave iteration
-#ifndef RT_SEG_FORM
-#define RT_SEG_FORM 3  // where a full spill region is resolved (rt_scan_kernel)
-#endif
 constexpr uint32_t CONT16 = 0x8000u;
 constexpr uint32_t CONT32 = 0x80000000u;
 constexpr uint32_t T3H_VALID = 1u << 24;
@@ -1009,12 +1006,14 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 // region, walked after the chunk loop, with whether their
                 // placeholder (t12 of the key) is nonzero
                 uint32_t room = kRounds ? RT_QCAP - qn - rr.keep : 0u;
-#if RT_SEG_FORM == 3
-                if (__builtin_expect(sn + (total - room) > scap, 0)) {  // the region could overflow: resolve it first
+                // the region could overflow: resolve it first (the test
+                // sits here, off the random-text path; in the chunk loop
+                // itself it measured ~1.5% slower on ids, and an outer
+                // loop of segments spilled 50 VGPRs in the u16 kernel)
+                if (__builtin_expect(sn + (total - room) > scap, 0)) {
                     resolve();
                     room = kRounds ? min(RT_QCAP, total) : 0u;
                 }
-#endif
                 uint32_t rank = base;
                 while (mm) {
                     const uint32_t j = __builtin_ctz(mm);
@@ -1054,7 +1053,6 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     if (kFilter && kRounds) issue(rr, 0);
     stand_in_store();
     if (!EF) fetch(xb, pb, ch + cstep);
-#if RT_SEG_FORM == 3
     for (;;) {  // wave-uniform
         if (ch >= cend) break;
         chunk(xa, pa, ch);
@@ -1063,37 +1061,6 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         ch += 2 * cstep;
     }
     resolve();
-#elif RT_SEG_FORM == 1
-    for (;;) {  // wave-uniform
-        if (ch >= cend) break;
-        chunk(xa, pa, ch);
-        if (ch + cstep >= cend) break;
-        chunk(xb, pb, ch + cstep);
-        ch += 2 * cstep;
-        // (scalar test) the region could overflow within the next two chunks
-        if (__builtin_expect(sn + 2 * RT_CHUNK > scap, 0)) resolve();
-    }
-    resolve();
-#else
-    for (bool done = false; !done;) {  // wave-uniform: segments, each ending in resolve()
-        for (;;) {
-            if (ch >= cend) {
-                done = true;
-                break;
-            }
-            chunk(xa, pa, ch);
-            if (ch + cstep >= cend) {
-                done = true;
-                break;
-            }
-            chunk(xb, pb, ch + cstep);
-            ch += 2 * cstep;
-            // (scalar test) the region could overflow within the next two chunks
-            if (__builtin_expect(sn + 2 * RT_CHUNK > scap, 0)) break;
-        }
-        resolve();
-    }
-#endif
     // the (at most two) chunks that touch the stream start or the tail: one
     // position per thread of the last workgroup (a chunk is 1024 positions),
     // so each costs one walk's latency, not sixteen
