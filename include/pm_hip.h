@@ -203,6 +203,10 @@ void pm_hip_debug_dfa_variant(int v);
  * LDS rows, 3 / 4 = (1) with two segments per lane; -1 = the product choice
  * (2 for ids, 0 for count only). */
 void pm_hip_debug_dfa_lds(int v);
+/* Tests only: the reverse-trie kernel's spill region bound per wave, in
+ * 1024-position chunks (>= 1; 0 = the default 16), so a small launch
+ * resolves full regions many times. */
+void pm_hip_debug_spill_cap(int chunks);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

@@ -23,6 +23,9 @@ struct RtDev {
 // RtDev::spill: one per position of each wave's chunks.  Launches of any n reuse one buffer of
 // this size for n' <= n.
 int64_t pm_rt_spill_items(int64_t n, int num_cu);
+// Tests: the spill region's bound per wave in chunks (>= 1; 0 restores the
+// default), so small launches resolve full regions many times.
+void pm_rt_set_spill_cap(int chunks);
 
 struct DfaDev {
     const uint32_t* next;  // states * 256 (output-coded when coded, pm_flatten.h)

@@ -1735,11 +1735,13 @@ static int64_t rt_blocks(int64_t n, int num_cu) {
 #define RT_SPILL_CAP_CHUNKS 16
 #endif
 constexpr int64_t RT_SPILL_WAVE_CAP = RT_SPILL_CAP_CHUNKS * RT_CHUNK;
+static int64_t g_spill_cap = RT_SPILL_WAVE_CAP;  // pm_rt_set_spill_cap (tests: >= one chunk)
 static int64_t rt_spill_stride(int64_t n, int64_t blocks) {
     const int64_t nw = blocks * RT_WAVES;
     const int64_t natural = ((n / RT_CHUNK + nw - 1) / nw) * RT_CHUNK;
-    return natural < RT_SPILL_WAVE_CAP ? natural : RT_SPILL_WAVE_CAP;
+    return natural < g_spill_cap ? natural : g_spill_cap;
 }
+void pm_rt_set_spill_cap(int chunks) { g_spill_cap = chunks >= 1 ? (int64_t)chunks * RT_CHUNK : RT_SPILL_WAVE_CAP; }
 
 int64_t pm_rt_spill_items(int64_t n, int num_cu) {
     constexpr int64_t PIECE = (int64_t)RT_POSMASK + 1;

@@ -824,6 +824,39 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     assert len(set(zip(kernels[5:], forms[5:]))) == 1, (kernels, forms)
 
 
+@pytest.mark.parametrize("cap", [1, 2])
+def test_bounded_spill_region_resolves_many_times(cap):
+    """The RT spill region is bounded per wave (pm_kernels.hip, resolved in
+    the push's ring-full branch when a chunk could overflow it).  With the
+    bound at 1-2 chunks, 32 MiB of the shipped stream (deep matches: a
+    quarter of the positions spill) resolves full regions dozens of times
+    per wave; ids (u32, u16) and counts equal the AC-DFA's."""
+    import torch
+    lib = pm.load()
+    n = 32 << 20
+    text = _tiled_ship(n)
+    dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    matcher("merged", "ac").scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s)
+    rt = matcher("merged", "rt")
+    lib.pm_hip_debug_spill_cap(cap)
+    try:
+        got = torch.empty(n, dtype=torch.int32, device="cuda")
+        got16 = torch.empty(n, dtype=torch.int16, device="cuda")
+        c = torch.zeros(3, dtype=torch.int64, device="cuda")
+        rt.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), c[0:].data_ptr(), s)
+        rt.scan_device(dt.data_ptr(), 0, 0, n, got16.data_ptr(), c[1:].data_ptr(), s, out_width=2)
+        rt.scan_device(dt.data_ptr(), 0, 0, n, None, c[2:].data_ptr(), s)
+        torch.cuda.synchronize()
+    finally:
+        lib.pm_hip_debug_spill_cap(0)
+    assert torch.equal(got, want)
+    assert torch.equal(got16.to(torch.int32) & 0xFFFF, want)
+    nz = int((want != 0).sum().item())
+    assert c.tolist() == [nz, nz, nz]
+
+
 def test_auto_scan_device_across_two_streams_and_hold():
     """The auto kind's pick is polled, never waited for (pm_plugin.hip
     launch): launches alternating between two streams with no host
