@@ -207,6 +207,9 @@ void pm_hip_debug_dfa_lds(int v);
  * 1024-position chunks (>= 1; 0 = the default 16), so a small launch
  * resolves full regions many times. */
 void pm_hip_debug_spill_cap(int chunks);
+/* Timing sweeps only: at most b workgroups per reverse-trie launch (0 = one
+ * per CU). */
+void pm_hip_debug_rt_blocks(int b);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

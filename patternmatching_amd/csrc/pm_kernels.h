@@ -26,6 +26,7 @@ int64_t pm_rt_spill_items(int64_t n, int num_cu);
 // Tests: the spill region's bound per wave in chunks (>= 1; 0 restores the
 // default), so small launches resolve full regions many times.
 void pm_rt_set_spill_cap(int chunks);
+void pm_rt_set_max_blocks(int b);  // timing sweeps: RT workgroups per launch (0 = one per CU)
 
 struct DfaDev {
     const uint32_t* next;  // states * 256 (output-coded when coded, pm_flatten.h)

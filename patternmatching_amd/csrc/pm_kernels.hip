@@ -1719,11 +1719,14 @@ __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint6
 
 // Workgroups of an RT launch over n positions (persistent: one 1024-lane
 // workgroup per CU, LDS-bound) and the spill items its waves may need.
+static int g_rt_max_blocks = 0;  // pm_rt_set_max_blocks (timing sweeps); 0 = one per CU
 static int64_t rt_blocks(int64_t n, int num_cu) {
     const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
     const int64_t blocks = (nchunks + RT_WAVES - 1) / RT_WAVES;
-    return blocks > num_cu ? num_cu : (blocks < 1 ? 1 : blocks);
+    const int64_t cap = g_rt_max_blocks > 0 && g_rt_max_blocks < num_cu ? g_rt_max_blocks : num_cu;
+    return blocks > cap ? cap : (blocks < 1 ? 1 : blocks);
 }
+void pm_rt_set_max_blocks(int b) { g_rt_max_blocks = b > 0 ? b : 0; }
 // Spill items per wave region: one per position of the wave's main-loop
 // chunks, capped at RT_SPILL_WAVE_CAP (the kernel resolves a full region
 // and goes on, rt_scan_kernel): 128 KiB per wave, 512 MiB for a 1 GiB launch

@@ -20,11 +20,13 @@ ap.add_argument("--stream", type=int, default=0, help="0 ascii, 1 bytes, 2 the s
 ap.add_argument("--variants", default="0,1,2")
 ap.add_argument("--modes", default="dense,dense16,count")
 ap.add_argument("--exact", default="", help="variants whose dense u32 ids must equal v0's (checked after timing)")
+ap.add_argument("--blocks", type=int, default=0, help="RT workgroups per launch (pm_hip_debug_rt_blocks; 0 = one per CU)")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 WIDTH = {"dense": 4, "dense16": 2, "count": 0}
 data = os.path.join(REPO, "tests", "golden", "data")
 lib = pm.load()
+lib.pm_hip_debug_rt_blocks(args.blocks)
 d = pm.Dictionary([os.path.join(data, x) for x in DICTS[args.dict]])
 m = pm.HipMatcher("rt")
 m.add_dictionary(d)
