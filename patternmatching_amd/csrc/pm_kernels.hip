@@ -1719,12 +1719,26 @@ __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint6
 
 // Workgroups of an RT launch over n positions (persistent: one 1024-lane
 // workgroup per CU, LDS-bound) and the spill items its waves may need.
-static int g_rt_max_blocks = 0;  // pm_rt_set_max_blocks (timing sweeps); 0 = one per CU
+// Workgroups: one per CU for large launches; a small launch gives each
+// wave at least 8 chunks, but keeps a quarter of the CUs (each workgroup
+// stages 80-160 KiB of tables into LDS, a fixed cost that swamps one or two
+// chunks per wave).  Side by side on et (ms, profiles/r03/rt_grid_sweep.json):
+//   4 MiB: 32 / 64 / 128 / 256 workgroups 0.036 / 0.027 / 0.035 / 0.059
+//   16 MiB:                              0.101 / 0.058 / 0.049 / 0.067
+//   64 MiB:                              0.366 / 0.193 / 0.116 / 0.104
+static int g_rt_max_blocks = 0;  // pm_rt_set_max_blocks (timing sweeps); 0 = the rule above
 static int64_t rt_blocks(int64_t n, int num_cu) {
     const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
-    const int64_t blocks = (nchunks + RT_WAVES - 1) / RT_WAVES;
-    const int64_t cap = g_rt_max_blocks > 0 && g_rt_max_blocks < num_cu ? g_rt_max_blocks : num_cu;
-    return blocks > cap ? cap : (blocks < 1 ? 1 : blocks);
+    if (g_rt_max_blocks > 0) {
+        const int64_t b = (nchunks + RT_WAVES - 1) / RT_WAVES, cap = g_rt_max_blocks < num_cu ? g_rt_max_blocks : num_cu;
+        return b > cap ? cap : (b < 1 ? 1 : b);
+    }
+    const int64_t one_each = (nchunks + RT_WAVES - 1) / RT_WAVES;     // one chunk per wave
+    const int64_t eight_each = (nchunks + 8 * RT_WAVES - 1) / (8 * RT_WAVES);
+    const int64_t floor_b = one_each < num_cu / 4 ? one_each : num_cu / 4;
+    int64_t b = eight_each > floor_b ? eight_each : floor_b;
+    if (b > num_cu) b = num_cu;
+    return b < 1 ? 1 : b;
 }
 void pm_rt_set_max_blocks(int b) { g_rt_max_blocks = b > 0 ? b : 0; }
 // Spill items per wave region: one per position of the wave's main-loop

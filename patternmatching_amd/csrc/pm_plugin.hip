@@ -121,6 +121,20 @@ struct PipeSlot {
     size_t off = 0, m = 0;  // block = positions [off, off + m) of the call
 };
 
+// RT scratch of the scan_device launches on one stream.  Launches on one
+// stream are ordered, so they share it; launches on different streams may
+// run at once, so each stream has its own (two launches sharing one wrote
+// each other's spill items).  Past PM_STREAM_SCRATCH streams the least
+// recently used one is handed over, behind an event wait on its last launch.
+constexpr size_t PM_STREAM_SCRATCH = 4;
+struct StreamSpill {
+    hipStream_t s = nullptr;
+    uint32_t* buf = nullptr;
+    int64_t cap = 0;
+    hipEvent_t done = nullptr;  // recorded after each launch on s
+    uint64_t used = 0;
+};
+
 struct PmHip {
     int kind_req = KIND_RT;
     int kind = 0;
@@ -141,8 +155,10 @@ struct PmHip {
     bool cache_hit = false;
     std::vector<void*> allocs;
     size_t table_bytes = 0;
-    uint32_t* spill = nullptr;  // RT deep-walk scratch of scan_device launches
+    uint32_t* spill = nullptr;  // RT deep-walk scratch of captured scan_device launches (graphs)
     int64_t spill_cap = 0;
+    std::vector<StreamSpill> sspill;  // ... and of direct ones, per stream (stream_spill)
+    uint64_t sspill_tick = 0;
     // streaming: the carried history (the last stream bytes, at least
     // max_len of them) and a two-slot pipeline (scan_host)
     PmHistRing hist;
@@ -214,8 +230,9 @@ void free_slot(PipeSlot& q) {
 // of each wave's chunks up to a bound per wave (the kernel resolves a full
 // region and goes on), so a launch of any size needs at most
 // pm_rt_spill_items(INT64_MAX) items: 512 MiB on 256 CUs.  compile()
-// allocates that for scan_device launches, so no launch frees or
-// allocates (hipFree synchronizes the device); read_block slots size theirs
+// allocates that for captured scan_device launches, which may not allocate;
+// a stream's scratch (stream_spill) grows to its largest launch (a hipFree
+// synchronizes the device, once per size step); read_block slots size theirs
 // to their block.  Scratch, not part of the automaton's total_mem.
 void ensure_spill(PmHip* o, uint32_t*& buf, int64_t& cap, int64_t n) {
     if (o->kind != KIND_RT && o->kind != KIND_AUTO) return;
@@ -225,6 +242,31 @@ void ensure_spill(PmHip* o, uint32_t*& buf, int64_t& cap, int64_t n) {
     buf = nullptr;
     PM_CHECK(hipMalloc(&buf, (size_t)need * 2 * sizeof(uint32_t)));  // 8-B items
     cap = need;
+}
+
+// The scratch of a direct (not captured) scan_device launch of n positions
+// on stream s; nullptr for a kind without the RT kernel.
+StreamSpill* stream_spill(PmHip* o, hipStream_t s, int64_t n) {
+    if (o->kind != KIND_RT && o->kind != KIND_AUTO) return nullptr;
+    StreamSpill* e = nullptr;
+    for (StreamSpill& x : o->sspill)
+        if (x.s == s) e = &x;
+    if (!e && o->sspill.size() < PM_STREAM_SCRATCH) {
+        o->sspill.emplace_back();
+        e = &o->sspill.back();
+        e->s = s;
+        PM_CHECK(hipEventCreateWithFlags(&e->done, hipEventDisableTiming));
+    }
+    if (!e) {  // hand over the least recently used one, after its last launch
+        e = &o->sspill[0];
+        for (StreamSpill& x : o->sspill)
+            if (x.used < e->used) e = &x;
+        PM_CHECK(hipStreamWaitEvent(s, e->done, 0));
+        e->s = s;
+    }
+    e->used = ++o->sspill_tick;
+    ensure_spill(o, e->buf, e->cap, n);
+    return e;
 }
 
 void ensure_slot(PmHip* o, PipeSlot& q, size_t positions) {
@@ -674,6 +716,10 @@ void pm_hip_free(void* obj) {
     (void)hipSetDevice(o->device);
     for (void* p : o->allocs) (void)hipFree(p);
     if (o->spill) (void)hipFree(o->spill);
+    for (StreamSpill& x : o->sspill) {
+        if (x.buf) (void)hipFree(x.buf);
+        if (x.done) (void)hipEventDestroy(x.done);
+    }
     if (o->d_lines_pats) (void)hipFree(o->d_lines_pats);
     if (o->d_lines_offs) (void)hipFree(o->d_lines_offs);
     free_pick(o->pick);
@@ -718,9 +764,17 @@ static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
     }
     hipError_t e = hipSetDevice(o->device);
     if (e == hipSuccess) {
-        ensure_spill(o, o->spill, o->spill_cap, n);
-        e = launch(o, d_text, stream_start, pos0, n, d_out, outw, d_count, (hipStream_t)hip_stream, o->spill,
-                   o->spill_cap, o->pick);
+        // a captured launch keeps the compile-time scratch (a graph owns the
+        // pointers it was captured with: replays of graphs of one object run
+        // one at a time, as any graph's scratch); a direct one its stream's
+        const hipStream_t s = (hipStream_t)hip_stream;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        e = hipStreamIsCapturing(s, &cs);
+        StreamSpill* sp = e == hipSuccess && cs == hipStreamCaptureStatusNone ? stream_spill(o, s, n) : nullptr;
+        if (e == hipSuccess)
+            e = launch(o, d_text, stream_start, pos0, n, d_out, outw, d_count, s, sp ? sp->buf : o->spill,
+                       sp ? sp->cap : o->spill_cap, o->pick);
+        if (e == hipSuccess && sp) e = hipEventRecord(sp->done, s);
         o->last_kernel = o->pick.last ? o->pick.last : o->kind;
         o->last_form = o->pick.last_form;
     }

@@ -857,6 +857,36 @@ def test_bounded_spill_region_resolves_many_times(cap):
     assert c.tolist() == [nz, nz, nz]
 
 
+def test_rt_scan_device_concurrent_streams_spill():
+    """Launches of one RT object on different streams may run at once; each
+    stream has its own spill scratch (pm_plugin.hip stream_spill), and past
+    four streams the least recently used one is handed over behind an event
+    wait.  Deep input with the region bounded at two chunks per wave makes
+    every launch use its scratch; six streams, launched with no host
+    synchronization, must all be exact."""
+    import torch
+    n = 6 << 20
+    text = _tiled_ship(n)
+    dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    ref = matcher("et", "ac")
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    lib = pm.load()
+    lib.pm_hip_debug_spill_cap(2)
+    try:
+        m = matcher("et", "rt")
+        streams = [torch.cuda.Stream() for _ in range(6)]
+        outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(18)]
+        for k, o in enumerate(outs):
+            m.scan_device(dt.data_ptr(), 0, 0, n, o.data_ptr(), None, streams[k % 6].cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        lib.pm_hip_debug_spill_cap(0)
+    for o in outs:
+        assert torch.equal(o, want)
+
+
 def test_auto_scan_device_across_two_streams_and_hold():
     """The auto kind's pick is polled, never waited for (pm_plugin.hip
     launch): launches alternating between two streams with no host
