@@ -1457,8 +1457,11 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
     return *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
 }
 
-template <int OUTW, int BLK, int KR, int CH = 1>
-__global__ __launch_bounds__(DFA_LDS_THREADS) void dfa_sparse_lds_kernel(
+// WPE: the waves per SIMD the register allocation must allow (0: the
+// compiler's choice); each more resident workgroup is 512 more chains per CU
+template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0>
+__global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
+void dfa_sparse_lds_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
     const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len) {
@@ -1496,13 +1499,15 @@ __global__ __launch_bounds__(DFA_LDS_THREADS) void dfa_sparse_lds_kernel(
             s[k] = 0;
             wmax = lo[k] - wlo[k] > wmax ? lo[k] - wlo[k] : wmax;
         }
+        // (every loop over the chains k is unrolled in the front end: R[k]
+        // must never be indexed at run time, or the arrays go to scratch)
         for (int64_t j = wmax; j > 0; --j) {  // warm-up from the root, right-aligned
-#pragma unroll
-            for (int k = 0; k < CH; ++k) {
+            unroll_for<0, CH>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
                 const bool on = lo[k] - j >= wlo[k];
                 const uint32_t v = sdfa_lds_step<KR>(base, F, s_rows, s[k], on ? text[lo[k] - j] : 0u, cb[k], R[k]);
                 s[k] = on ? v & DFA_STATE_MASK : s[k];
-            }
+            });
         }
         constexpr int NW = BLK / 4;
         const int64_t nblk = seg_len / BLK;
@@ -1525,17 +1530,18 @@ __global__ __launch_bounds__(DFA_LDS_THREADS) void dfa_sparse_lds_kernel(
                 }
             }
             if (!any) break;
-            uint32_t code[CH][BLK], st[CH][BLK];
+            // the coded words themselves (target | code << 20): one register
+            // per position holds both the code and, for an escape, the state
+            uint32_t vw[CH][BLK];
 #pragma unroll
             for (int j = 0; j < BLK; ++j) {
-#pragma unroll
-                for (int k = 0; k < CH; ++k) {
+                unroll_for<0, CH>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
                     const uint32_t v =
                         sdfa_lds_step<KR>(base, F, s_rows, s[k], (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb[k], R[k]);
                     s[k] = act[k] ? v & DFA_STATE_MASK : s[k];
-                    code[k][j] = v >> 20;
-                    st[k][j] = s[k];
-                }
+                    vw[k][j] = v;
+                });
             }
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
@@ -1543,7 +1549,8 @@ __global__ __launch_bounds__(DFA_LDS_THREADS) void dfa_sparse_lds_kernel(
                 uint32_t r[BLK];
                 // (count only: an escape code is a nonzero id, no lookup)
 #pragma unroll
-                for (int j = 0; j < BLK; ++j) r[j] = OUTW && code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
+                for (int j = 0; j < BLK; ++j)
+                    r[j] = OUTW && (vw[k][j] >> 20) == DFA_ESC ? outt[vw[k][j] & DFA_STATE_MASK] : vw[k][j] >> 20;
                 const int64_t i = lo[k] + BLK * b;
                 if (OUTW == 4) {
                     uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
@@ -1562,15 +1569,17 @@ __global__ __launch_bounds__(DFA_LDS_THREADS) void dfa_sparse_lds_kernel(
                 for (int j = 0; j < BLK; ++j) cnt += r[j] != 0u;
             }
         }
-#pragma unroll
-        for (int k = 0; k < CH; ++k) {  // the segments' last (< BLK) positions
+        // the segments' last (< BLK) positions; k a compile-time constant
+        // (a runtime k would index R[k] dynamically: the array goes to scratch)
+        unroll_for<0, CH>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
             for (int64_t i = lo[k] + BLK * ((hi[k] - lo[k]) / BLK); i < hi[k]; ++i) {
                 s[k] = sdfa_lds_step<KR>(base, F, s_rows, s[k], text[i], cb[k], R[k]) & DFA_STATE_MASK;
                 const uint32_t v = outt[s[k]];
                 if (OUTW) put_id<OUTW>(out, i - pos0, v);
                 cnt += v != 0u;
             }
-        }
+        });
     }
     if (count) {
         for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
@@ -1908,7 +1917,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
     const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw ? 2 : 0;
-    const bool lds2 = sparse && sdfa_lds >= 3 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
+    const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const int64_t lanes = (int64_t)num_cu * g_dfa_lanes_per_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
@@ -1925,7 +1934,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains) {
         // one workgroup of DFA_LDS_THREADS lanes per CU, persistent over
         // the segments (the LDS rows are staged once per workgroup)
-        const int lch = sdfa_lds >= 3 ? 2 : 1;
+        const int lch = sdfa_lds >= 3 && sdfa_lds <= 6 ? 2 : 1;
         int64_t wg = (nseg + DFA_LDS_THREADS * lch - 1) / (DFA_LDS_THREADS * lch);
         const int64_t cap = (int64_t)num_cu * g_dfa_lanes_per_cu / DFA_LDS_THREADS;
         if (wg > cap) wg = cap;
@@ -1933,6 +1942,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         const dim3 g2((unsigned)wg), b2(DFA_LDS_THREADS);
 #define DL(W, B, K, C)                                                                                               \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, K, C>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
+                       t.sbase, t.sF, t.sout, t.warm, seg)
+#define DLW(W, B, E)                                                                                                 \
+    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, 0, 1, E>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
                        t.sbase, t.sF, t.sout, t.warm, seg)
         switch (sdfa_lds) {
             case 2:  // the register record blocks alone (timing)
@@ -1946,11 +1958,27 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                 if (outw == 4) DL(4, 32, DFA_LDS_ROWS, 2); else if (outw == 2) DL(2, 32, DFA_LDS_ROWS, 2);
                 else DL(0, 32, DFA_LDS_ROWS, 2);
                 break;
+            case 5:  // record blocks, two segments per lane
+                if (outw == 4) DL(4, 32, 0, 2); else if (outw == 2) DL(2, 32, 0, 2); else DL(0, 32, 0, 2);
+                break;
+            case 6:
+                if (outw == 4) DL(4, 16, 0, 2); else if (outw == 2) DL(2, 16, 0, 2); else DL(0, 16, 0, 2);
+                break;
+            case 7:  // record blocks, 16-position blocks (fewer registers: more waves per SIMD)
+                if (outw == 4) DL(4, 16, 0, 1); else if (outw == 2) DL(2, 16, 0, 1); else DL(0, 16, 0, 1);
+                break;
+            case 8:  // the same, registers capped for 6 waves per SIMD (three workgroups per CU)
+                if (outw == 4) DLW(4, 16, 6); else if (outw == 2) DLW(2, 16, 6); else DLW(0, 16, 8);
+                break;
+            case 9:  // 32-position blocks, registers capped for 6 waves per SIMD
+                if (outw == 4) DLW(4, 32, 6); else if (outw == 2) DLW(2, 32, 6); else DLW(0, 32, 8);
+                break;
             default:
                 if (outw == 4) DL(4, 32, DFA_LDS_ROWS, 1); else if (outw == 2) DL(2, 32, DFA_LDS_ROWS, 1);
                 else DL(0, 32, DFA_LDS_ROWS, 1);
         }
 #undef DL
+#undef DLW
         return hipGetLastError();
     }
     if (sparse) {
@@ -2025,7 +2053,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 4 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 9 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }
