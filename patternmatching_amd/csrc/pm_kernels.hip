@@ -41,6 +41,9 @@
 //   step is one 16-B load (a row's quad, or the record) plus, at a record
 //   whose two bytes miss, one 4-B load of the fallback's row.  The plugin
 //   times both forms and keeps the faster per input (pm_plugin.hip).
+//   Product kernel of the form: dfa_sparse_lds_kernel without LDS rows --
+//   each lane keeps the aligned block of 4 records holding its state in
+//   registers -- at two 512-lane workgroups per CU.
 #include <type_traits>
 
 #include <algorithm>
@@ -1521,8 +1524,8 @@ void dfa_sparse_lds_kernel(
                 any |= act[k];
 #pragma unroll
                 for (int q = 0; q < BLK / 16; ++q) {
-                    const uint4 w = act[k] ? *reinterpret_cast<const uint4*>(text + lo[k] + BLK * b + 16 * q)
-                                           : make_uint4(0u, 0u, 0u, 0u);
+                    const tu32x4 w = act[k] ? *reinterpret_cast<const tu32x4*>(text + lo[k] + BLK * b + 16 * q)
+                                            : tu32x4{0u, 0u, 0u, 0u};
                     W[k][4 * q] = w.x;
                     W[k][4 * q + 1] = w.y;
                     W[k][4 * q + 2] = w.z;
@@ -1857,6 +1860,7 @@ hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream
 // more distinct table lines than the caches hold.
 constexpr int DFA_LANES_PER_CU = 512;
 static int g_dfa_lanes_per_cu = DFA_LANES_PER_CU;
+static bool g_dfa_shape_forced = false;  // pm_dfa_set_shape: every form at the swept lanes
 // Shortest segment.  A launch of fewer segments than lanes is latency-bound
 // (each lane's chain of max_len-1 warm-up + segment dependent steps is the
 // launch time), so short launches want short segments, at the price of
@@ -1890,9 +1894,13 @@ static int g_dfa_dense_blk = DFA_DENSE_BLK;
 static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64-position blocks)
 // The sparse form's kernel: 0 = dfa_sparse_kernel, 1 = dfa_sparse_lds_kernel
 // (LDS rows + register record blocks), 2 = the latter without LDS rows,
-// 3 / 4 = (1) with two segments per lane (16 / 32-position blocks); -1 =
-// the product choice: 2 for ids, 0 for count only.  Side by side (snort, 1
-// GiB, ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json):
+// 3 / 4 = (1) with two segments per lane (16 / 32-position blocks), 5 / 6 =
+// (2) with two segments per lane, 7 = (2) with 16-position blocks, 8 = (7)
+// with registers capped for 6 waves per SIMD; -1 = the product choice: 2,
+// at SDFA_LANES_PER_CU.  Side by side at 512 lanes per CU (snort, 1 GiB,
+// ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
+// rows are the round's first two-segment build, whose register arrays the
+// compiler had put in scratch):
 //            lines dense / count   shipped dense / count   ASCII dense / count
 //   0         9.64 / 8.05          10.04 / 5.82            6.25 / 4.85
 //   1         9.82 / 8.77           8.69 / 6.05            6.09 / 5.06
@@ -1903,6 +1911,29 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // 0.72 G per launch, all of them L2 hits), but the L2 misses -- the table
 // lines that come from the Infinity Cache or HBM, 0.39 G per launch either
 // way -- are what the kernel waits for; two segments per lane double them.
+// What does move it is the number of chains a CU keeps in flight: (2) holds
+// a position's coded word in one register (118 VGPRs: 4 waves per SIMD), so
+// two 512-lane workgroups fit a CU.  Lanes per CU (profiles/r03/
+// sdfa_lanes_*.txt, sdfa_occupancy_sweep.txt; dense u32 / count only, ms):
+//                 lines          shipped        ASCII
+//   (2) x 512     9.43 / 8.28    8.57 / 5.83    7.13 / --
+//   (2) x 1024    8.89 / 6.73    5.77 / 4.74    7.19 / 5.95
+//   (2) x 1536    10.19 / 8.39   7.37 / 6.26    7.86 / 6.76   (6 WGs on 4 slots)
+//   (8) x 1536    11.53 / 9.03   8.14 / 6.63    8.87 / 7.25   (3 resident WGs)
+//   (0) x 512     9.17 / 8.02    8.74 / 5.61
+// Past two workgroups per CU every stream slows down, resident or not:
+// the table gathers then saturate the memory system.  Two segments per
+// lane at 512 lanes (5 / 6, no scratch now) measured 10.3 / 10.75 ms on
+// the lines stream.  Measured and removed (profiles/r03/
+// sdfa_pipelined_ids_ab.txt, lines / shipped / ASCII, dense u32): (2) with
+// non-temporal id stores 11.9 / 8.9 / 8.9 ms against 9.0 / 5.8 / 7.2; the
+// ids of block b resolved and stored one 16-B chunk per step of block b + 1
+// (so the escape lookups and the stores would overlap the next table loads
+// instead of stalling a block's end) 13.1 / 8.5 / 9.7: a store interleaved
+// with the steps puts its L2 acknowledgement on the chain (vmcnt retires in
+// order) at steps whose table load is a register or L2 hit, eight times a
+// block instead of once.
+constexpr int SDFA_LANES_PER_CU = 1024;
 static int g_sdfa_lds = -1;
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
@@ -1916,10 +1947,12 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw ? 2 : 0;
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : 2;
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
-    const int64_t lanes = (int64_t)num_cu * g_dfa_lanes_per_cu;
+    const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
+    const int lanes_cu = g_dfa_shape_forced || !lds_kernel ? g_dfa_lanes_per_cu : SDFA_LANES_PER_CU;
+    const int64_t lanes = (int64_t)num_cu * lanes_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
@@ -1931,12 +1964,12 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), b(DFA_THREADS);
-    if (sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains) {
+    if (lds_kernel) {
         // one workgroup of DFA_LDS_THREADS lanes per CU, persistent over
         // the segments (the LDS rows are staged once per workgroup)
         const int lch = sdfa_lds >= 3 && sdfa_lds <= 6 ? 2 : 1;
         int64_t wg = (nseg + DFA_LDS_THREADS * lch - 1) / (DFA_LDS_THREADS * lch);
-        const int64_t cap = (int64_t)num_cu * g_dfa_lanes_per_cu / DFA_LDS_THREADS;
+        const int64_t cap = lanes / DFA_LDS_THREADS;
         if (wg > cap) wg = cap;
         if (wg < 1) wg = 1;
         const dim3 g2((unsigned)wg), b2(DFA_LDS_THREADS);
@@ -1970,12 +2003,6 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             case 8:  // the same, registers capped for 6 waves per SIMD (three workgroups per CU)
                 if (outw == 4) DLW(4, 16, 6); else if (outw == 2) DLW(2, 16, 6); else DLW(0, 16, 8);
                 break;
-            case 9:  // 32-position blocks, registers capped for 6 waves per SIMD
-                if (outw == 4) DLW(4, 32, 6); else if (outw == 2) DLW(2, 32, 6); else DLW(0, 32, 8);
-                break;
-            default:
-                if (outw == 4) DL(4, 32, DFA_LDS_ROWS, 1); else if (outw == 2) DL(2, 32, DFA_LDS_ROWS, 1);
-                else DL(0, 32, DFA_LDS_ROWS, 1);
         }
 #undef DL
 #undef DLW
@@ -2045,7 +2072,10 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     return hipGetLastError();
 }
 
-void pm_dfa_set_shape(int lanes_per_cu) { g_dfa_lanes_per_cu = lanes_per_cu > 0 ? lanes_per_cu : DFA_LANES_PER_CU; }
+void pm_dfa_set_shape(int lanes_per_cu) {
+    g_dfa_lanes_per_cu = lanes_per_cu > 0 ? lanes_per_cu : DFA_LANES_PER_CU;
+    g_dfa_shape_forced = lanes_per_cu > 0;
+}
 void pm_dfa_set_min_seg(int min_seg) { g_dfa_min_seg = min_seg >= 16 ? min_seg : 0; }
 void pm_dfa_set_sparse(int sparse) { g_dfa_sparse = sparse < 0 ? -1 : sparse != 0; }
 void pm_dfa_set_block(int blk) {
@@ -2053,7 +2083,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 9 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 8 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }

@@ -722,6 +722,50 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
         lib.pm_hip_debug_dfa_block(0)
 
 
+@pytest.mark.parametrize("stream", ["lines", "ship"])
+def test_sparse_dfa_kernel_variants_agree(stream):
+    """Every kernel of the sparse form (pm_hip_debug_dfa_lds 0-8: plain, LDS
+    rows, register record blocks, two segments per lane, 16-position blocks,
+    capped registers)
+    at 512 / 1024 / 1536 lanes per CU gives the RT
+    kernel's u32 / u16 ids and the same count, at sizes from one warm-up
+    segment to 32 MiB (snort)."""
+    torch = _torch()
+    lib = pm.load()
+    rt, ac = matcher("snort", "rt"), matcher("snort", "ac")
+    n = 32 << 20
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    if stream == "lines":
+        rt.gen_lines_device(dt.data_ptr(), n + 64, 11, s)
+    else:
+        dt.copy_(torch.from_numpy(np.tile(SHIP, (n + 64) // len(SHIP) + 1)[: n + 64]).cuda())
+    ref = torch.empty(n, dtype=torch.int32, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, ref.data_ptr(), None, s)
+    lib.pm_hip_debug_dfa_sparse(1)
+    try:
+        for size, start in ((n, 0), (777, 4096), (100 << 10, 12345 & ~15), (5 << 20, 3 << 20)):
+            for form in range(9):
+                for lanes in ((512, 1024, 1536) if form in (2, 8) else (0,)):
+                    lib.pm_hip_debug_dfa_lds(form)
+                    lib.pm_hip_debug_dfa_shape(lanes)
+                    a = torch.zeros(size, dtype=torch.int32, device="cuda")
+                    h = torch.zeros(size, dtype=torch.int16, device="cuda")
+                    c = torch.zeros(2, dtype=torch.int64, device="cuda")
+                    ac.scan_device(dt.data_ptr(), 0, start, size, a.data_ptr(), c[0:1].data_ptr(), s)
+                    ac.scan_device(dt.data_ptr(), 0, start, size, h.data_ptr(), None, s, out_width=2)
+                    ac.scan_device(dt.data_ptr(), 0, start, size, 0, c[1:2].data_ptr(), s)
+                    torch.cuda.synchronize()
+                    tag = (size, form, lanes)
+                    assert torch.equal(a, ref[start:start + size]), tag
+                    assert torch.equal(h.to(torch.int32) & 0xFFFF, a), tag
+                    assert int(c[0].item()) == int(c[1].item()) == int((a != 0).sum().item()), tag
+    finally:
+        lib.pm_hip_debug_dfa_lds(-1)
+        lib.pm_hip_debug_dfa_shape(0)
+        lib.pm_hip_debug_dfa_sparse(-1)
+
+
 def test_adversarial_stream_large_rt_equals_ac():
     """A 32 MiB tiling of the shipped adversarial stream queues far more
     positions than the worklist holds, so the scan kernel's in-kernel
