@@ -891,20 +891,30 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
 #define RT_RAW(j) ((uint32_t)((((uint64_t)x[(j) >> 2].y << 32) | x[(j) >> 2].x) >> (8 * (2 + ((j) & 3)))))
 #define RT_KEY(j) (RT_RAW(j) & 0xFFFFFFu)
         uint32_t res[16];
-        uint32_t cm = 0;  // bit j: position j goes past depth 2
+        // bit j << CMS: position j goes past depth 2 (count only keeps two
+        // bits per position, the candidate bit is the odd one)
+        constexpr int CMS = kT8 ? 1 : 0;
+        uint32_t cm = 0;
         if (kT8) {
-            // count only: zero answers under a node with children are queued
-            // (cand, bit 1); the nonzero ones (bit 0) are counted per lane
-            // from the sum of the 16 classes (sum = nz + 2 cand): one add per
-            // position instead of a compare, a ballot and two scalar ops
-            uint32_t sum = 0;
+            // count only: the 16 classes {nz, cand} of the lane's positions
+            // side by side in one word, two bits each -- the key (text[i] <<
+            // 8 | text[i-1], the byte address of the class) by one v_perm, the
+            // class shifted into place by one v_lshl_or: two VALU per
+            // position.  Nonzero answers (even bits) are counted per lane;
+            // zero answers under a node with children (odd bits) are queued.
+            // Against the class sum (5 VALU per position), side by side:
+            // random ASCII 0.455 -> 0.432 ms, shipped 0.637 -> 0.600, lines
+            // 0.879 -> 0.862 (profiles/r03/count_perm_staging_ab.txt).
+            uint32_t f = 0;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const uint32_t v = s_t8[(RT_RAW(j) >> 8) & 0xFFFFu];
-                cm |= (v >> 1) << j;
-                sum += v;
+                constexpr uint32_t kSel0 = 0x0C0C0000u;  // bytes 2, 3 = 0; byte 1 = text[i], byte 0 = text[i-1]
+                const uint32_t b = (uint32_t)(j & 3);
+                const uint32_t key = __builtin_amdgcn_perm(x[j >> 2].y, x[j >> 2].x, kSel0 | (4u + b) << 8 | (3u + b));
+                f |= (uint32_t)s_t8[key] << (2 * j);
             }
-            cnt += sum - 2u * (uint32_t)__popc(cm);
+            cnt += (uint32_t)__popc(f & 0x55555555u);
+            cm = f & 0xAAAAAAAAu;
         } else {
 #pragma unroll
         for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
@@ -992,7 +1002,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 // i-3..i by one 64-bit shift
                 uint32_t slot = qh + qn + base;
                 while (mm) {
-                    const uint32_t j = __builtin_ctz(mm);
+                    const uint32_t j = __builtin_ctz(mm) >> CMS;
                     mm &= mm - 1;
                     const uint32_t sg = j >> 2, b = j & 3;
                     const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
@@ -1019,7 +1029,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 }
                 uint32_t rank = base;
                 while (mm) {
-                    const uint32_t j = __builtin_ctz(mm);
+                    const uint32_t j = __builtin_ctz(mm) >> CMS;
                     mm &= mm - 1;
                     const uint32_t sg = j >> 2, b = j & 3;
                     const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
