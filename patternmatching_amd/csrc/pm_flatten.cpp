@@ -428,6 +428,42 @@ static void build_sparse(DfaImage& im, const BfsTrie& t, const std::vector<uint3
     }
 }
 
+bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vector<uint32_t>& out8) {
+    const uint32_t F = d.sF, S = d.states;
+    if (d.sblock.empty() || F < 1 || F >= (1u << 22)) return false;
+    const uint32_t* rec = d.sblock.data() + (size_t)F * 256;
+    std::vector<uint32_t> nid(S);
+    for (uint32_t v = 0; v < F; ++v) nid[v] = v;
+    uint64_t u = 0;  // next free unit
+    for (uint32_t v = F; v < S; ++v) {
+        const bool two = (rec[(size_t)(v - F) * 4] & 0x1000000u) != 0;
+        if (two && (u & 7) == 7) ++u;  // keep both units in one 64-B block
+        nid[v] = F + (uint32_t)u;
+        u += two ? 2 : 1;
+        if (F + u > PM_DFA_STATE_MASK + 1) return false;
+    }
+    auto remap = [&](uint32_t w) { return nid[w & PM_DFA_STATE_MASK] | (w & ~PM_DFA_STATE_MASK); };
+    block8.assign((size_t)F * 256 + 2 * u, 0);
+    out8.assign(F + u, 0);
+    for (size_t e = 0; e < (size_t)F * 256; ++e) block8[e] = remap(d.sblock[e]);
+    for (uint32_t v = 0; v < S; ++v) out8[nid[v]] = d.sout[v];
+    for (uint32_t v = F; v < S; ++v) {
+        const uint32_t* R = rec + (size_t)(v - F) * 4;  // {x, y, z, w}
+        uint32_t* U = &block8[(size_t)F * 256 + 2 * (size_t)(nid[v] - F)];
+        const uint32_t y = (R[0] & 0x100u) ? remap(R[1]) : 0u;
+        if (R[0] & 0x1000000u) {
+            U[0] = y;
+            U[1] = R[0] | 0x80000000u;
+            U[2] = remap(R[2]);
+            U[3] = R[3];
+        } else {
+            U[0] = y;
+            U[1] = (R[0] & 0x1FFu) | R[3] << 9;
+        }
+    }
+    return true;
+}
+
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
     DfaImage im;
     BfsTrie t = build_trie(pats, g, /*reversed=*/false, PM_DFA_DFS_DEPTH);

@@ -150,6 +150,20 @@ RtImage pm_build_rt(const std::vector<std::string>& pats, const PmGidMap& g);
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g);
 PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap& g);
 
+// The sparse form with 8-B record units (a device layout, built from the
+// 16-B form at compile time; not cached): rows [0, F) as before, then the
+// records in the same order, each at a unit offset u with state id F + u:
+//   zero or one slot (75% of snort's records): one unit {y, x0 | w << 9},
+//     x0 = c0 | 0x100 (0: no slot), w = the fallback row;
+//   two slots: two units {y, x | 1 << 31}, {z, w} (x as in the 16-B
+//     form), never straddling an aligned 64-B block of 8 units (a padding
+//     unit before it when it would).
+// Every coded word's target is renumbered; out8 is indexed by the new ids
+// (padding ids 0).  A walk along a pattern's unary run reads twice as many
+// states per line as with 16-B records.  False when the new ids do not fit
+// the coded word's 20-bit target field.
+bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vector<uint32_t>& out8);
+
 // Compiled-image cache: the flattened tables of a
 // dictionary, on disk, keyed by a hash of the patterns in add order and the
 // image kind.  pm_image_key hashes (format version, kind, the layout

@@ -36,6 +36,8 @@ struct DfaDev {
     const uint8_t* sbase;  // sparse form (coded only): rows | records block, pm_flatten.h
     const uint32_t* sout;  // states, the sparse numbering
     uint32_t sF;           // states with full rows
+    const uint8_t* sbase8;  // the same with 8-B record units (pm_pack_sparse8), or null
+    const uint32_t* sout8;  // its ids' outputs
     int form;              // 0 = the default (pm_dfa_set_sparse), 1 = dense rows, 2 = sparse
 };
 

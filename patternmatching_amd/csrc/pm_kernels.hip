@@ -1442,12 +1442,16 @@ __device__ __forceinline__ uint4 pick4(const uint4 (&R)[4], uint32_t k) {
     return (k & 2u) ? b : a;
 }
 
-template <int KR>
+// RB: record bytes.  16: the 16-B form, 4 records per 64-B block.  8: the
+// 8-B unit form (pm_pack_sparse8), 8 units per block: a one-slot record is
+// one unit {y, x0 | w << 9}, a two-slot record two {y, x | 1 << 31}, {z, w}
+// in the same block.
+template <int KR, int RB = 16>
 __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ base, uint32_t F,
                                                   const uint32_t* __restrict__ s_rows, uint32_t s, uint32_t c,
                                                   uint32_t& cb, uint4 (&R)[4]) {
     const bool isrow = s < F;
-    const uint32_t rec = s - F, b = rec >> 2;
+    const uint32_t rec = s - F, b = rec >> (RB == 8 ? 3 : 2);
     uint32_t rv = 0;
     if (isrow) {
         if (KR && s < (uint32_t)KR) rv = s_rows[s * 256u + c];
@@ -1461,8 +1465,22 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
         cb = b;
     }
     if (isrow) return rv;
-    const uint4 q = pick4(R, rec & 3u);
     const uint32_t key = c | 0x100u;
+    if (RB == 8) {
+        const uint32_t e = rec & 7u;
+        const uint4 q = pick4(R, e >> 1), q2 = pick4(R, ((e >> 1) + 1u) & 3u);
+        const uint32_t y = (e & 1u) ? q.z : q.x, x = (e & 1u) ? q.w : q.y;
+        if ((x & 0x1FFu) == key) return y;
+        uint32_t w = (x >> 9) & 0x3FFFFFu;
+        if (x >> 31) {
+            const uint32_t z = (e & 1u) ? q2.x : q.z;
+            if (((x >> 16) & 0x1FFu) == key) return z;
+            w = (e & 1u) ? q2.y : q.w;
+        }
+        if (KR && w < (uint32_t)KR) return s_rows[w * 256u + c];
+        return *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
+    }
+    const uint4 q = pick4(R, rec & 3u);
     if ((q.x & 0x1FFu) == key) return q.y;
     if (((q.x >> 16) & 0x1FFu) == key) return q.z;
     const uint32_t w = q.w;  // the fallback row
@@ -1472,7 +1490,7 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
 
 // WPE: the waves per SIMD the register allocation must allow (0: the
 // compiler's choice); each more resident workgroup is 512 more chains per CU
-template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0>
+template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0, int RB = 16>
 __global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void dfa_sparse_lds_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
@@ -1518,7 +1536,7 @@ void dfa_sparse_lds_kernel(
             unroll_for<0, CH>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 const bool on = lo[k] - j >= wlo[k];
-                const uint32_t v = sdfa_lds_step<KR>(base, F, s_rows, s[k], on ? text[lo[k] - j] : 0u, cb[k], R[k]);
+                const uint32_t v = sdfa_lds_step<KR, RB>(base, F, s_rows, s[k], on ? text[lo[k] - j] : 0u, cb[k], R[k]);
                 s[k] = on ? v & DFA_STATE_MASK : s[k];
             });
         }
@@ -1551,7 +1569,7 @@ void dfa_sparse_lds_kernel(
                 unroll_for<0, CH>([&](auto kc) {
                     constexpr int k = decltype(kc)::value;
                     const uint32_t v =
-                        sdfa_lds_step<KR>(base, F, s_rows, s[k], (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb[k], R[k]);
+                        sdfa_lds_step<KR, RB>(base, F, s_rows, s[k], (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb[k], R[k]);
                     s[k] = act[k] ? v & DFA_STATE_MASK : s[k];
                     vw[k][j] = v;
                 });
@@ -1587,7 +1605,7 @@ void dfa_sparse_lds_kernel(
         unroll_for<0, CH>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             for (int64_t i = lo[k] + BLK * ((hi[k] - lo[k]) / BLK); i < hi[k]; ++i) {
-                s[k] = sdfa_lds_step<KR>(base, F, s_rows, s[k], text[i], cb[k], R[k]) & DFA_STATE_MASK;
+                s[k] = sdfa_lds_step<KR, RB>(base, F, s_rows, s[k], text[i], cb[k], R[k]) & DFA_STATE_MASK;
                 const uint32_t v = outt[s[k]];
                 if (OUTW) put_id<OUTW>(out, i - pos0, v);
                 cnt += v != 0u;
@@ -1906,8 +1924,9 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // (LDS rows + register record blocks), 2 = the latter without LDS rows,
 // 3 / 4 = (1) with two segments per lane (16 / 32-position blocks), 5 / 6 =
 // (2) with two segments per lane, 7 = (2) with 16-position blocks, 8 = (7)
-// with registers capped for 6 waves per SIMD; -1 = the product choice: 2,
-// at SDFA_LANES_PER_CU.  Side by side at 512 lanes per CU (snort, 1 GiB,
+// with registers capped for 6 waves per SIMD, 9 = (2) over the 8-B record
+// units of pm_pack_sparse8 (2 when the automaton has none); -1 = the
+// product choice: 9, at SDFA_LANES_PER_CU.  Side by side at 512 lanes per CU (snort, 1 GiB,
 // ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
 // rows are the round's first two-segment build, whose register arrays the
 // compiler had put in scratch):
@@ -1934,7 +1953,12 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // Past two workgroups per CU every stream slows down, resident or not:
 // the table gathers then saturate the memory system.  Two segments per
 // lane at 512 lanes (5 / 6, no scratch now) measured 10.3 / 10.75 ms on
-// the lines stream.  Measured and removed (profiles/r03/
+// the lines stream.  8-B record units (9; 75% of snort's records are one
+// unit, so a 128-B line holds twice the states of a pattern's run) against
+// (2) at 1024 lanes, side by side (profiles/r03/sdfa_units8_ab.txt; dense /
+// u16 / count, ms): lines 9.04 / 8.58 / 6.83 -> 8.42 / 7.93 / 6.73, shipped
+// 5.83 / 5.32 / 4.75 -> 5.85 / 5.47 / 4.80, ASCII 7.22 / 6.87 / 5.96 ->
+// 7.20 / 6.89 / 6.01.  Measured and removed (profiles/r03/
 // sdfa_pipelined_ids_ab.txt, lines / shipped / ASCII, dense u32): (2) with
 // non-temporal id stores 11.9 / 8.9 / 8.9 ms against 9.0 / 5.8 / 7.2; the
 // ids of block b resolved and stored one 16-B chunk per step of block b + 1
@@ -1957,7 +1981,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : 2;
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : 9;
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
@@ -1986,6 +2010,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #define DL(W, B, K, C)                                                                                               \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, K, C>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
                        t.sbase, t.sF, t.sout, t.warm, seg)
+#define DL8(W)                                                                                                    \
+    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, 0, 1, 0, 8>), g2, b2, 0, s, text, stream_start, pos0, n, out,  \
+                       count, t.sbase8, t.sF, t.sout8, t.warm, seg)
 #define DLW(W, B, E)                                                                                                 \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, 0, 1, E>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
                        t.sbase, t.sF, t.sout, t.warm, seg)
@@ -2010,12 +2037,21 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             case 7:  // record blocks, 16-position blocks (fewer registers: more waves per SIMD)
                 if (outw == 4) DL(4, 16, 0, 1); else if (outw == 2) DL(2, 16, 0, 1); else DL(0, 16, 0, 1);
                 break;
+            case 9:  // (2) over the 8-B record units (pm_pack_sparse8)
+                if (!t.sbase8) {
+                    if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
+                } else if (outw == 4) DL8(4); else if (outw == 2) DL8(2); else DL8(0);
+                break;
             case 8:  // the same, registers capped for 6 waves per SIMD (three workgroups per CU)
                 if (outw == 4) DLW(4, 16, 6); else if (outw == 2) DLW(2, 16, 6); else DLW(0, 16, 8);
                 break;
+            default:  // 1: LDS rows + record blocks
+                if (outw == 4) DL(4, 32, DFA_LDS_ROWS, 1); else if (outw == 2) DL(2, 32, DFA_LDS_ROWS, 1);
+                else DL(0, 32, DFA_LDS_ROWS, 1);
         }
 #undef DL
 #undef DLW
+#undef DL8
         return hipGetLastError();
     }
     if (sparse) {
@@ -2093,7 +2129,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 8 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 9 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }

@@ -630,6 +630,12 @@ void pm_hip_compile(void* obj) {
             im.dfa.sblock.resize(im.dfa.sblock.size() - 16);
             o->dfa.sout = (const uint32_t*)dalloc_copy(o, im.dfa.sout.data(), im.dfa.sout.size() * 4);
             o->dfa.sF = im.dfa.sF;
+            std::vector<uint32_t> b8, o8;  // the 8-B record units (pm_pack_sparse8)
+            if (pm_pack_sparse8(im.dfa, b8, o8)) {
+                b8.resize(b8.size() + 16, 0u);  // the last aligned 64-B block
+                o->dfa.sbase8 = (const uint8_t*)dalloc_copy(o, b8.data(), b8.size() * 4);
+                o->dfa.sout8 = (const uint32_t*)dalloc_copy(o, o8.data(), o8.size() * 4);
+            }
         }
     }
     // read_char's host step keeps the RT image (rt / auto), or the DFA's
@@ -983,6 +989,7 @@ struct PmFlatHandle {
     RtImage rt;
     DfaImage dfa;
     PmParents par;
+    std::vector<uint32_t> block8, out8;  // pm_pack_sparse8 of the DFA's sparse form
     int kind = 0;
     bool hit = false;
 };
@@ -1001,6 +1008,7 @@ void* pm_flat_build_cached(const char* const* pats, const uint32_t* lens, size_t
     h->rt = std::move(im.rt);
     h->dfa = std::move(im.dfa);
     h->par = std::move(im.par);
+    if (!pm_pack_sparse8(h->dfa, h->block8, h->out8)) h->block8.clear(), h->out8.clear();
     return h;
 }
 
@@ -1031,6 +1039,8 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
     if (s == "out") return ret(h->dfa.out);
     if (s == "sblock") return ret(h->dfa.sblock);
     if (s == "sout") return ret(h->dfa.sout);
+    if (s == "sblock8") return ret(h->block8);
+    if (s == "sout8") return ret(h->out8);
     if (s == "index_of_gid") return ret(h->g.index_of_gid);
     if (s == "parent") return ret(h->par.parent);
     if (s == "depth") return ret(h->par.depth);

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <fstream>
 #include <list>
 #include <map>
@@ -78,9 +79,10 @@ int main(int argc, char** argv) {
         std::sort(fr.begin(), fr.end(), [](auto a, auto b) { return a.first > b.first; });
         for (int r = 0; r < 256; ++r) perm[fr[r].second] = r;
     }
-    for (int pm : {0, 1})
-    for (int regrec : {4}) {
-        for (size_t chains : {16384ul, 32768ul}) {
+    const int RECB = getenv("RECB") ? atoi(getenv("RECB")) : 16;  // record bytes (8: an upper bound on 8-B unary records)
+    for (int pm : {0})
+    for (int regrec : {64 / RECB}) {
+        for (size_t chains : {32768ul}) {
             memset(g_cmiss, 0, sizeof g_cmiss);
             const size_t per = 1024;  // bytes per chain
             const size_t SEG = 8192;                  // the real segment spacing (1 GiB / 131072 lanes)
@@ -117,7 +119,7 @@ int main(int argc, char** argv) {
                         tbl += cnt;
                         v = B[(size_t)s * 256 + c];
                     } else {
-                        const uint64_t off = (uint64_t)F * 1024 + (uint64_t)(s - F) * 16;
+                        const uint64_t off = (uint64_t)F * 1024 + (uint64_t)(s - F) * RECB;
                         const uint32_t blk = (s - F) / regrec;
                         g_cat = 1;
                         if (blk != cb[L] || regrec == 1) {

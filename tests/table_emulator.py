@@ -227,6 +227,47 @@ def sdfa_scan(img, text):
     return res
 
 
+def sdfa8_scan(img, text):
+    """dfa_sparse_lds_kernel<..., RB = 8> over the 8-B record units
+    (pm_pack_sparse8, pm_flatten.h): rows as in the 16-B form; state F + u
+    is the record at unit u -- {y, x0 | w << 9} with one or no slot, or
+    {y, x | 1 << 31}, {z, w} with two, never straddling an aligned block of
+    8 units.  Codes checked against sout8 at every step."""
+    F = int(img.lib.pm_flat_dfa_sparse_rows(img.h))
+    blk = img.array("sblock8")
+    sout = img.array("sout8")
+    assert F >= 1 and len(blk) == F * 256 + (len(sout) - F) * 2
+    rows = blk[: F * 256]
+    units = blk[F * 256:].reshape(-1, 2)
+    s = 0
+    res = np.empty(len(text), np.uint32)
+    for j, c in enumerate(np.asarray(text, dtype=np.uint8).tolist()):
+        if s < F:
+            x = int(rows[s * 256 + c])
+        else:
+            u = s - F
+            y, xw = int(units[u][0]), int(units[u][1])
+            key = c | 0x100
+            if xw & 0x1FF == key:
+                x = y
+            elif xw >> 31 and (xw >> 16) & 0x1FF == key:
+                assert u % 8 != 7  # both units in one 64-B block
+                x = int(units[u + 1][0])
+            else:
+                if xw >> 31:
+                    assert u % 8 != 7
+                    w = int(units[u + 1][1])
+                else:
+                    w = (xw >> 9) & 0x3FFFFF
+                assert w < F
+                x = int(rows[w * 256 + c])
+        s = x & 0xFFFFF
+        code = x >> 20
+        assert code == min(int(sout[s]), 4095)
+        res[j] = code if code != 4095 else sout[s]
+    return res
+
+
 def gid_to_code(img, dictionary):
     idx = img.array("index_of_gid")
     codes = dictionary.codes()

@@ -9,7 +9,7 @@ import pytest
 
 import patternmatching_amd as pm
 from oracle_lib import DATA, GOLDEN, dict_paths, oracle_for
-from table_emulator import FlatImage, dfa_scan, filter2_maybe, filter_maybe, gid_to_code, rt_scan, sdfa_scan
+from table_emulator import FlatImage, dfa_scan, filter2_maybe, filter_maybe, gid_to_code, rt_scan, sdfa8_scan, sdfa_scan
 
 MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
 SHIP = np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8)
@@ -247,6 +247,21 @@ def test_dfa_image_ship_stream(key):
     gold = np.fromfile(os.path.join(GOLDEN, f"ship_{key}.u32"), dtype="<u4")
     assert np.array_equal(tab[dfa_scan(img, SHIP)], gold)
     assert np.array_equal(tab[sdfa_scan(img, SHIP)], gold)
+    assert np.array_equal(tab[sdfa8_scan(img, SHIP)], gold)
+
+
+@pytest.mark.parametrize("key", ["et", "snort"])
+def test_sparse8_units_lines_stream(key):
+    """The 8-B record units (pm_pack_sparse8): the same answers as the 16-B
+    form on the dictionary's own lines stream (deep, unary runs), and most
+    records take one unit."""
+    d, img, tab = image(key, pm.KIND_AC)
+    F = int(img.lib.pm_flat_dfa_sparse_rows(img.h))
+    S = len(img.array("sout"))
+    units = (len(img.array("sblock8")) - F * 256) // 2
+    assert S - F < units < 1.5 * (S - F)
+    text = d.gen_lines(1 << 15, 4)
+    assert np.array_equal(sdfa8_scan(img, text), sdfa_scan(img, text))
 
 
 @pytest.mark.parametrize("key,mode", [("et", 0), ("snort", 1)])
@@ -262,6 +277,7 @@ def test_sparse_dfa_image_random(key, mode):
     o = oracle_for(key)
     o.reset()
     assert np.array_equal(tab[sdfa_scan(img, text)], o.scan_codes(text))
+    assert np.array_equal(tab[sdfa8_scan(img, text)], o.scan_codes(text))
 
 
 def test_small_dictionaries():
@@ -297,3 +313,4 @@ def test_small_dictionaries():
         assert np.array_equal(tab[rt_scan(img, text)], exp), pats[:3]
         assert np.array_equal(dtab[dfa_scan(dimg, text)], exp), pats[:3]
         assert np.array_equal(dtab[sdfa_scan(dimg, text)], exp), pats[:3]
+        assert np.array_equal(dtab[sdfa8_scan(dimg, text)], exp), pats[:3]
