@@ -1490,7 +1490,7 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
 
 // WPE: the waves per SIMD the register allocation must allow (0: the
 // compiler's choice); each more resident workgroup is 512 more chains per CU
-template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0, int RB = 16>
+template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0, int RB = 16, int TB = 1>
 __global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void dfa_sparse_lds_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
@@ -1542,25 +1542,38 @@ void dfa_sparse_lds_kernel(
         }
         constexpr int NW = BLK / 4;
         const int64_t nblk = seg_len / BLK;
-        for (int64_t b = 0; b < nblk; ++b) {
-            bool act[CH];
-            bool any = false;
-            uint32_t W[CH][NW];
+        // the text of TB consecutive blocks per load: with TB = 2 a lane's
+        // 128-B line of text is fetched twice instead of four times (it is
+        // evicted between blocks: 1,024 chains per CU step through the L2)
+        for (int64_t b0 = 0; b0 < nblk; b0 += TB) {
+            bool actt[TB][CH], anyt[TB];
+            uint32_t WT[TB][CH][NW];
 #pragma unroll
-            for (int k = 0; k < CH; ++k) {
-                act[k] = lo[k] + BLK * b + BLK <= hi[k];
-                any |= act[k];
+            for (int tt = 0; tt < TB; ++tt) {
+                anyt[tt] = false;
 #pragma unroll
-                for (int q = 0; q < BLK / 16; ++q) {
-                    const tu32x4 w = act[k] ? *reinterpret_cast<const tu32x4*>(text + lo[k] + BLK * b + 16 * q)
-                                            : tu32x4{0u, 0u, 0u, 0u};
-                    W[k][4 * q] = w.x;
-                    W[k][4 * q + 1] = w.y;
-                    W[k][4 * q + 2] = w.z;
-                    W[k][4 * q + 3] = w.w;
+                for (int k = 0; k < CH; ++k) {
+                    actt[tt][k] = lo[k] + BLK * (b0 + tt) + BLK <= hi[k];
+                    anyt[tt] |= actt[tt][k];
+#pragma unroll
+                    for (int q = 0; q < BLK / 16; ++q) {
+                        const tu32x4 w = actt[tt][k]
+                                             ? *reinterpret_cast<const tu32x4*>(text + lo[k] + BLK * (b0 + tt) + 16 * q)
+                                             : tu32x4{0u, 0u, 0u, 0u};
+                        WT[tt][k][4 * q] = w.x;
+                        WT[tt][k][4 * q + 1] = w.y;
+                        WT[tt][k][4 * q + 2] = w.z;
+                        WT[tt][k][4 * q + 3] = w.w;
+                    }
                 }
             }
-            if (!any) break;
+            if (!anyt[0]) break;
+            unroll_for<0, TB>([&](auto tc) {
+            constexpr int tt = decltype(tc)::value;
+            if (tt > 0 && !anyt[tt]) return;
+            const int64_t b = b0 + tt;
+            const bool(&act)[CH] = actt[tt];
+            const uint32_t(&W)[CH][NW] = WT[tt];
             // the coded words themselves (target | code << 20): one register
             // per position holds both the code and, for an escape, the state
             uint32_t vw[CH][BLK];
@@ -1599,6 +1612,7 @@ void dfa_sparse_lds_kernel(
 #pragma unroll
                 for (int j = 0; j < BLK; ++j) cnt += r[j] != 0u;
             }
+            });
         }
         // the segments' last (< BLK) positions; k a compile-time constant
         // (a runtime k would index R[k] dynamically: the array goes to scratch)
@@ -1925,8 +1939,9 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // 3 / 4 = (1) with two segments per lane (16 / 32-position blocks), 5 / 6 =
 // (2) with two segments per lane, 7 = (2) with 16-position blocks, 8 = (7)
 // with registers capped for 6 waves per SIMD, 9 = (2) over the 8-B record
-// units of pm_pack_sparse8 (2 when the automaton has none); -1 = the
-// product choice: 9, at SDFA_LANES_PER_CU.  Side by side at 512 lanes per CU (snort, 1 GiB,
+// units of pm_pack_sparse8 (2 when the automaton has none), 10 = (9) with
+// the text of two blocks per load; -1 = the product choice: 10, at
+// SDFA_LANES_PER_CU.  Side by side at 512 lanes per CU (snort, 1 GiB,
 // ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
 // rows are the round's first two-segment build, whose register arrays the
 // compiler had put in scratch):
@@ -1958,7 +1973,10 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // (2) at 1024 lanes, side by side (profiles/r03/sdfa_units8_ab.txt; dense /
 // u16 / count, ms): lines 9.04 / 8.58 / 6.83 -> 8.42 / 7.93 / 6.73, shipped
 // 5.83 / 5.32 / 4.75 -> 5.85 / 5.47 / 4.80, ASCII 7.22 / 6.87 / 5.96 ->
-// 7.20 / 6.89 / 6.01.  Measured and removed (profiles/r03/
+// 7.20 / 6.89 / 6.01.  Two blocks' text per load (10 against 9; 128 VGPRs,
+// still 4 waves; profiles/r03/sdfa_text_two_blocks_ab.txt): lines 8.36 /
+// 7.93 / 6.71 -> 8.16 / 7.72 / 6.49, shipped 5.88 / 5.48 / 4.73 -> 5.76 /
+// 5.33 / 4.63, ASCII dense 7.20 -> 6.97.  Measured and removed (profiles/r03/
 // sdfa_pipelined_ids_ab.txt, lines / shipped / ASCII, dense u32): (2) with
 // non-temporal id stores 11.9 / 8.9 / 8.9 ms against 9.0 / 5.8 / 7.2; the
 // ids of block b resolved and stored one 16-B chunk per step of block b + 1
@@ -1981,7 +1999,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : 9;
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : 10;
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
@@ -2013,6 +2031,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #define DL8(W)                                                                                                    \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, 0, 1, 0, 8>), g2, b2, 0, s, text, stream_start, pos0, n, out,  \
                        count, t.sbase8, t.sF, t.sout8, t.warm, seg)
+#define DL8T(W)                                                                                                      \
+    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, 0, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
+                       count, t.sbase8, t.sF, t.sout8, t.warm, seg)
 #define DLW(W, B, E)                                                                                                 \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, 0, 1, E>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
                        t.sbase, t.sF, t.sout, t.warm, seg)
@@ -2042,6 +2063,11 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                     if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
                 } else if (outw == 4) DL8(4); else if (outw == 2) DL8(2); else DL8(0);
                 break;
+            case 10:  // (9) with the text of two blocks per load
+                if (!t.sbase8) {
+                    if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
+                } else if (outw == 4) DL8T(4); else if (outw == 2) DL8T(2); else DL8T(0);
+                break;
             case 8:  // the same, registers capped for 6 waves per SIMD (three workgroups per CU)
                 if (outw == 4) DLW(4, 16, 6); else if (outw == 2) DLW(2, 16, 6); else DLW(0, 16, 8);
                 break;
@@ -2052,6 +2078,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #undef DL
 #undef DLW
 #undef DL8
+#undef DL8T
         return hipGetLastError();
     }
     if (sparse) {
@@ -2129,7 +2156,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 9 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 10 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }
