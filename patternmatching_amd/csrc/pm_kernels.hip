@@ -1940,7 +1940,8 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // (2) with two segments per lane, 7 = (2) with 16-position blocks, 8 = (7)
 // with registers capped for 6 waves per SIMD, 9 = (2) over the 8-B record
 // units of pm_pack_sparse8 (2 when the automaton has none), 10 = (9) with
-// the text of two blocks per load; -1 = the product choice: 10, at
+// the text of two blocks per load, 11 / 12 = (10) with the first 32 / 64
+// rows in LDS; -1 = the product choice: 12 for ids, 10 for count only, at
 // SDFA_LANES_PER_CU.  Side by side at 512 lanes per CU (snort, 1 GiB,
 // ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
 // rows are the round's first two-segment build, whose register arrays the
@@ -1976,7 +1977,13 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // 7.20 / 6.89 / 6.01.  Two blocks' text per load (10 against 9; 128 VGPRs,
 // still 4 waves; profiles/r03/sdfa_text_two_blocks_ab.txt): lines 8.36 /
 // 7.93 / 6.71 -> 8.16 / 7.72 / 6.49, shipped 5.88 / 5.48 / 4.73 -> 5.76 /
-// 5.33 / 4.63, ASCII dense 7.20 -> 6.97.  Measured and removed (profiles/r03/
+// 5.33 / 4.63, ASCII dense 7.20 -> 6.97.  The root and the 63 shallowest
+// rows staged in LDS (12, 64 KiB per workgroup, two still fit a CU) against
+// (10), side by side (profiles/r03/sdfa_lds_rows_units8_ab.txt; dense / u16
+// / count): lines 8.20 / 7.74 / 6.42 -> 8.12 / 7.70 / 6.61, shipped 5.75 /
+// 5.33 / 4.63 -> 5.69 / 5.21 / 4.51, ASCII 6.98 / -- / 5.67 -> 6.60 / -- /
+// 5.41; 32 rows (11) measured equal to (10).  Ids take the tile, count only
+// (whose lines stream it slows) does not.  Measured and removed (profiles/r03/
 // sdfa_pipelined_ids_ab.txt, lines / shipped / ASCII, dense u32): (2) with
 // non-temporal id stores 11.9 / 8.9 / 8.9 ms against 9.0 / 5.8 / 7.2; the
 // ids of block b resolved and stored one 16-B chunk per step of block b + 1
@@ -1999,7 +2006,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : 10;
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw ? 12 : 10;
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
@@ -2033,6 +2040,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                        count, t.sbase8, t.sF, t.sout8, t.warm, seg)
 #define DL8T(W)                                                                                                      \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, 0, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
+                       count, t.sbase8, t.sF, t.sout8, t.warm, seg)
+#define DL8K(W, K)                                                                                                    \
+    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, K, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
                        count, t.sbase8, t.sF, t.sout8, t.warm, seg)
 #define DLW(W, B, E)                                                                                                 \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, 0, 1, E>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
@@ -2068,6 +2078,16 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                     if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
                 } else if (outw == 4) DL8T(4); else if (outw == 2) DL8T(2); else DL8T(0);
                 break;
+            case 11:  // (10) with the first 32 / 64 rows (the root and the shallowest states) in LDS
+            case 12:
+                if (!t.sbase8) {
+                    if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
+                } else if (sdfa_lds == 11) {
+                    if (outw == 4) DL8K(4, 32); else if (outw == 2) DL8K(2, 32); else DL8K(0, 32);
+                } else {
+                    if (outw == 4) DL8K(4, 64); else if (outw == 2) DL8K(2, 64); else DL8K(0, 64);
+                }
+                break;
             case 8:  // the same, registers capped for 6 waves per SIMD (three workgroups per CU)
                 if (outw == 4) DLW(4, 16, 6); else if (outw == 2) DLW(2, 16, 6); else DLW(0, 16, 8);
                 break;
@@ -2079,6 +2099,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #undef DLW
 #undef DL8
 #undef DL8T
+#undef DL8K
         return hipGetLastError();
     }
     if (sparse) {
@@ -2156,7 +2177,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 10 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 12 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }

@@ -724,7 +724,7 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
 
 @pytest.mark.parametrize("stream", ["lines", "ship"])
 def test_sparse_dfa_kernel_variants_agree(stream):
-    """Every kernel of the sparse form (pm_hip_debug_dfa_lds 0-10: plain, LDS
+    """Every kernel of the sparse form (pm_hip_debug_dfa_lds 0-12: plain, LDS
     rows, register record blocks, two segments per lane, 16-position blocks,
     capped registers)
     at 512 / 1024 / 1536 lanes per CU gives the RT
@@ -745,8 +745,8 @@ def test_sparse_dfa_kernel_variants_agree(stream):
     lib.pm_hip_debug_dfa_sparse(1)
     try:
         for size, start in ((n, 0), (777, 4096), (100 << 10, 12345 & ~15), (5 << 20, 3 << 20)):
-            for form in range(11):
-                for lanes in ((512, 1024, 1536) if form in (2, 8, 9, 10) else (0,)):
+            for form in range(13):
+                for lanes in ((512, 1024, 1536) if form in (2, 8, 9, 10, 12) else (0,)):
                     lib.pm_hip_debug_dfa_lds(form)
                     lib.pm_hip_debug_dfa_shape(lanes)
                     a = torch.zeros(size, dtype=torch.int32, device="cuda")
