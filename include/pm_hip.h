@@ -200,9 +200,16 @@ void pm_hip_debug_dfa_block(int blk);
 void pm_hip_debug_dfa_variant(int v);
 /* Timing experiments only: the sparse AC-DFA form's kernel: 0 = the plain
  * kernel, 1 = LDS rows + register record blocks, 2 = record blocks without
- * LDS rows, 3 / 4 = (1) with two segments per lane; -1 = the product choice
- * (2 for ids, 0 for count only). */
+ * LDS rows, 3 / 4 = (1) with two segments per lane, 5 / 6 = (2) with two
+ * segments per lane, 7 / 8 = (2) with 16-position blocks (8: registers
+ * capped for 6 waves per SIMD), 9 = (2) over 8-B record units, 10 = (9)
+ * with two blocks' text per load, 11 / 12 = (10) with 32 / 64 rows in LDS;
+ * -1 = the product choice (12 for ids, 10 for count only). */
 void pm_hip_debug_dfa_lds(int v);
+/* Timing experiments only: 0 = every warm-up of the sparse form's product
+ * kernels starts max_len - 1 bytes back; 1 (default) = at the last
+ * synchronizing 3-gram (one in no pattern) when there is one. */
+void pm_hip_debug_dfa_sync(int on);
 /* Tests only: the reverse-trie kernel's spill region bound per wave, in
  * 1024-position chunks (>= 1; 0 = the default 16), so a small launch
  * resolves full regions many times. */

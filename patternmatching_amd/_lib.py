@@ -118,6 +118,7 @@ SIGNATURES = {
     "pm_hip_debug_dfa_block": (None, [ctypes.c_int]),
     "pm_hip_debug_dfa_variant": (None, [ctypes.c_int]),
     "pm_hip_debug_dfa_lds": (None, [ctypes.c_int]),
+    "pm_hip_debug_dfa_sync": (None, [ctypes.c_int]),
     "pm_hip_debug_spill_cap": (None, [ctypes.c_int]),
     "pm_hip_debug_rt_blocks": (None, [ctypes.c_int]),
     # host-only table images

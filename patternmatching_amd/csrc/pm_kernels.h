@@ -38,6 +38,13 @@ struct DfaDev {
     uint32_t sF;           // states with full rows
     const uint8_t* sbase8;  // the same with 8-B record units (pm_pack_sparse8), or null
     const uint32_t* sout8;  // its ids' outputs
+    // 2^24-bit set of the 3-byte strings occurring in some pattern (bit
+    // t[q] | t[q+1] << 8 | t[q+2] << 16), or null.  A 3-gram outside it is
+    // synchronizing: the state after it is the root's over those 3 bytes
+    // (every longer suffix would hold the 3-gram), so a segment's warm-up
+    // can start at the last one before the segment instead of max_len - 1
+    // bytes back.
+    const uint32_t* gram3;
     int form;              // 0 = the default (pm_dfa_set_sparse), 1 = dense rows, 2 = sparse
 };
 
@@ -64,8 +71,9 @@ void pm_dfa_set_sparse(int sparse);
 bool pm_dfa_forced_form();
 void pm_dfa_set_variant(int v);  // timing experiments of the sparse kernel (u32 ids, one chain)
 void pm_dfa_set_block(int blk);  // sparse form, one chain: positions per block (16 or 32)
-// sparse form's kernel (timing): 0 plain, 1 LDS rows + record blocks (default), 2 record blocks only
+// sparse form's kernel (timing; pm_hip_debug_dfa_lds)
 void pm_dfa_set_lds(int v);
+void pm_dfa_set_sync(int on);  // warm-ups from synchronizing 3-grams (timing; default on)
 bool pm_dfa_default_sparse();  // the form a launch with DfaDev::form 0 runs
 // counts[0..4] += success, partial, false_neg, false_pos, all_matches of algo
 // against real (n u32 gids each, 16-B aligned); parent/depth: PmParents.

@@ -1495,7 +1495,7 @@ __global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu
 void dfa_sparse_lds_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
-    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len) {
+    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 1];
     if (KR) {
         const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
@@ -1528,6 +1528,27 @@ void dfa_sparse_lds_kernel(
             wlo[k] = lo[k] - warm < stream_start ? stream_start : lo[k] - warm;
             if (sg >= nseg) wlo[k] = lo[k];
             s[k] = 0;
+            // start the warm-up at the last synchronizing 3-gram before lo
+            // (DfaDev::gram3: no pattern holds it, so the state after it is
+            // the root's over its 3 bytes), 16 candidates per round
+            if (gram3) {
+                bool found = false;
+                for (int64_t qh = lo[k] - 3; !found && qh >= wlo[k]; qh -= 16) {
+                    uint32_t absent = 0;  // bit u: the 3-gram at qh - u is in no pattern
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        const int64_t q = qh - u;
+                        if (q >= wlo[k]) {
+                            const uint32_t x = text[q] | (uint32_t)text[q + 1] << 8 | (uint32_t)text[q + 2] << 16;
+                            absent |= (~gram3[x >> 5] >> (x & 31) & 1u) << u;
+                        }
+                    }
+                    if (absent) {
+                        wlo[k] = qh - __builtin_ctz(absent);
+                        found = true;
+                    }
+                }
+            }
             wmax = lo[k] - wlo[k] > wmax ? lo[k] - wlo[k] : wmax;
         }
         // (every loop over the chains k is unrolled in the front end: R[k]
@@ -1994,6 +2015,9 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // block instead of once.
 constexpr int SDFA_LANES_PER_CU = 1024;
 static int g_sdfa_lds = -1;
+// warm-ups start at the last synchronizing 3-gram (forms 10 and 12; 0:
+// always max_len - 1 bytes back, timing)
+static int g_dfa_sync = 0;
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
 // does not name one (-1: not forced; the plugin then times both forms)
@@ -2032,21 +2056,22 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         if (wg > cap) wg = cap;
         if (wg < 1) wg = 1;
         const dim3 g2((unsigned)wg), b2(DFA_LDS_THREADS);
+        const uint32_t* g3 = g_dfa_sync ? t.gram3 : nullptr;  // synchronizing 3-grams (DfaDev::gram3)
 #define DL(W, B, K, C)                                                                                               \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, K, C>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
-                       t.sbase, t.sF, t.sout, t.warm, seg)
+                       t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr)
 #define DL8(W)                                                                                                    \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, 0, 1, 0, 8>), g2, b2, 0, s, text, stream_start, pos0, n, out,  \
-                       count, t.sbase8, t.sF, t.sout8, t.warm, seg)
+                       count, t.sbase8, t.sF, t.sout8, t.warm, seg, (const uint32_t*)nullptr)
 #define DL8T(W)                                                                                                      \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, 0, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
-                       count, t.sbase8, t.sF, t.sout8, t.warm, seg)
+                       count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
 #define DL8K(W, K)                                                                                                    \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, K, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
-                       count, t.sbase8, t.sF, t.sout8, t.warm, seg)
+                       count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
 #define DLW(W, B, E)                                                                                                 \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, 0, 1, E>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
-                       t.sbase, t.sF, t.sout, t.warm, seg)
+                       t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr)
         switch (sdfa_lds) {
             case 2:  // the register record blocks alone (timing)
                 if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
@@ -2180,6 +2205,7 @@ void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
 void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 12 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
+void pm_dfa_set_sync(int on) { g_dfa_sync = on != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }
 
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,

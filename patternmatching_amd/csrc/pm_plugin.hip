@@ -621,6 +621,16 @@ void pm_hip_compile(void* obj) {
         o->dfa.next = (const uint32_t*)dalloc_copy(o, im.dfa.next.data(), im.dfa.next.size() * 4);
         o->dfa.out = (const uint32_t*)dalloc_copy(o, im.dfa.out.data(), im.dfa.out.size() * 4);
         o->dfa.warm = o->max_len ? (int64_t)o->max_len - 1 : 0;
+        if (o->dfa.warm > 3) {  // the synchronizing 3-grams (DfaDev::gram3)
+            std::vector<uint32_t> g3((1u << 24) / 32, 0u);
+            for (const std::string& pt : o->pats)
+                for (size_t i = 0; i + 3 <= pt.size(); ++i) {
+                    const uint32_t x = (uint8_t)pt[i] | (uint32_t)(uint8_t)pt[i + 1] << 8 |
+                                       (uint32_t)(uint8_t)pt[i + 2] << 16;
+                    g3[x >> 5] |= 1u << (x & 31);
+                }
+            o->dfa.gram3 = (const uint32_t*)dalloc_copy(o, g3.data(), g3.size() * 4);
+        }
         o->dfa.coded = pm_dfa_coded(im.dfa.states) ? 1 : 0;
         if (!im.dfa.sblock.empty()) {
             // (+64 zero bytes: the LDS kernel reads records in aligned
@@ -878,6 +888,7 @@ void pm_hip_debug_dfa_sparse(int sparse) { pm_dfa_set_sparse(sparse); }
 void pm_hip_debug_dfa_block(int blk) { pm_dfa_set_block(blk); }
 void pm_hip_debug_dfa_variant(int v) { pm_dfa_set_variant(v); }
 void pm_hip_debug_dfa_lds(int v) { pm_dfa_set_lds(v); }
+void pm_hip_debug_dfa_sync(int on) { pm_dfa_set_sync(on); }
 void pm_hip_debug_spill_cap(int chunks) { pm_rt_set_spill_cap(chunks); }
 void pm_hip_debug_rt_blocks(int b) { pm_rt_set_max_blocks(b); }
 void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }

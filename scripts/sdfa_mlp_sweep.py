@@ -25,6 +25,7 @@ ap.add_argument("--streams", default="lines")
 ap.add_argument("--forms", default="2,5,6,0")
 ap.add_argument("--lanes", default="512,1024,1536,2048")
 ap.add_argument("--width", type=int, default=4, choices=[0, 2, 4])
+ap.add_argument("--sync", default="1", help="warm-ups from synchronizing 3-grams (pm_hip_debug_dfa_sync), e.g. 1,0")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 data = os.path.join(REPO, "tests", "golden", "data")
@@ -42,7 +43,8 @@ ref = torch.empty(n * max(w, 1) // 4 + 16, dtype=torch.int32, device="cuda")
 out = torch.empty_like(ref)
 cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
 res = {}
-settings = [(f, l) for f in map(int, args.forms.split(",")) for l in map(int, args.lanes.split(","))]
+settings = [(f, l, y) for f in map(int, args.forms.split(",")) for l in map(int, args.lanes.split(","))
+            for y in map(int, args.sync.split(","))]
 for st in args.streams.split(","):
     if st == "lines":
         m.gen_lines_device(text.data_ptr(), n + 64, 1, s.cuda_stream)
@@ -55,9 +57,10 @@ for st in args.streams.split(","):
     counts = {}
     for r in range(args.rounds + 1):
         for k in settings:
-            f, lanes = k
+            f, lanes, y = k
             lib.pm_hip_debug_dfa_lds(f)
             lib.pm_hip_debug_dfa_shape(lanes)
+            lib.pm_hip_debug_dfa_sync(y)
             cnt.zero_()
             dst = ref if k == settings[0] else out
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -70,13 +73,14 @@ for st in args.streams.split(","):
                 times[k].append(e0.elapsed_time(e1))
             counts[k] = int(cnt.item())
             if r == 0 and w and k != settings[0] and not torch.equal(out, ref):
-                raise SystemExit(f"{st}: form {f} lanes {lanes}: ids differ from {settings[0]}")
+                raise SystemExit(f"{st}: form {f} lanes {lanes} sync {y}: ids differ from {settings[0]}")
     assert len(set(counts.values())) == 1, counts
     for k in settings:
         ms = statistics.median(times[k])
-        res[f"{st}-f{k[0]}-L{k[1]}"] = {"ms": round(ms, 4), "stream_gbps": round(n / ms / 1e6, 1)}
-        print(f"{st} form {k[0]} lanes/CU {k[1]}: {ms:.3f} ms", flush=True)
+        res[f"{st}-f{k[0]}-L{k[1]}-y{k[2]}"] = {"ms": round(ms, 4), "stream_gbps": round(n / ms / 1e6, 1)}
+        print(f"{st} form {k[0]} lanes/CU {k[1]} sync {k[2]}: {ms:.3f} ms", flush=True)
 lib.pm_hip_debug_dfa_lds(-1)
 lib.pm_hip_debug_dfa_shape(0)
+lib.pm_hip_debug_dfa_sync(1)
 lib.pm_hip_debug_dfa_sparse(-1)
 print(json.dumps(res))

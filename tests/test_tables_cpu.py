@@ -314,3 +314,34 @@ def test_small_dictionaries():
         assert np.array_equal(dtab[dfa_scan(dimg, text)], exp), pats[:3]
         assert np.array_equal(dtab[sdfa_scan(dimg, text)], exp), pats[:3]
         assert np.array_equal(dtab[sdfa8_scan(dimg, text)], exp), pats[:3]
+
+
+@pytest.mark.parametrize("key", ["et", "snort"])
+def test_synchronizing_3gram_warmup(key):
+    """The sparse DFA kernels start a segment's warm-up at the last 3-gram
+    that occurs in no pattern (DfaDev::gram3): every suffix longer than it
+    would contain it, so the automaton state after it is the root's over
+    its 3 bytes.  Scanning from there gives the exact answers at every
+    position of the segment (oracle, from the stream start, on the
+    dictionary's lines stream and on the shipped stream)."""
+    d = pm.Dictionary(dict_paths(key))
+    grams = set()
+    for p in d.patterns():
+        for i in range(len(p) - 2):
+            grams.add(p[i:i + 3])
+    o = oracle_for(key)
+    warm = max(len(p) for p in d.patterns()) - 1
+    rng = np.random.default_rng(17)
+    for text in (d.gen_lines(1 << 16, 5), np.tile(SHIP, 7)[: 1 << 16]):
+        o.reset()
+        exact = o.scan_codes(text)
+        tb = text.tobytes()
+        synced = 0
+        for lo in rng.integers(warm + 8, len(text) - 600, size=60).tolist():
+            wlo = lo - warm
+            q = next((q for q in range(lo - 3, wlo - 1, -1) if tb[q:q + 3] not in grams), wlo)
+            synced += q != wlo
+            o.reset()
+            got = o.scan_codes(text[q:lo + 512])[lo - q:]
+            assert np.array_equal(got, exact[lo:lo + 512]), (lo, q)
+        assert synced > 0
