@@ -207,8 +207,8 @@ void pm_hip_debug_dfa_variant(int v);
  * -1 = the product choice (12 for ids, 10 for count only). */
 void pm_hip_debug_dfa_lds(int v);
 /* Timing experiments only: 0 = every warm-up of the sparse form's product
- * kernels starts max_len - 1 bytes back; 1 (default) = at the last
- * synchronizing 3-gram (one in no pattern) when there is one. */
+ * kernels starts max_len - 1 bytes back; 1 = at the last synchronizing
+ * 3-gram (one in no pattern) when there is one; -1 = the default. */
 void pm_hip_debug_dfa_sync(int on);
 /* Tests only: the reverse-trie kernel's spill region bound per wave, in
  * 1024-position chunks (>= 1; 0 = the default 16), so a small launch

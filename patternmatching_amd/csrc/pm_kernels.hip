@@ -2017,7 +2017,8 @@ constexpr int SDFA_LANES_PER_CU = 1024;
 static int g_sdfa_lds = -1;
 // warm-ups start at the last synchronizing 3-gram (forms 10 and 12; 0:
 // always max_len - 1 bytes back, timing)
-static int g_dfa_sync = 0;
+constexpr int kDfaSyncDefault = 0;
+static int g_dfa_sync = kDfaSyncDefault;
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
 // does not name one (-1: not forced; the plugin then times both forms)
@@ -2205,7 +2206,7 @@ void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
 void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 12 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
-void pm_dfa_set_sync(int on) { g_dfa_sync = on != 0; }
+void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }
 void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }
 
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,

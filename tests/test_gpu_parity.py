@@ -745,10 +745,12 @@ def test_sparse_dfa_kernel_variants_agree(stream):
     lib.pm_hip_debug_dfa_sparse(1)
     try:
         for size, start in ((n, 0), (777, 4096), (100 << 10, 12345 & ~15), (5 << 20, 3 << 20)):
-            for form in range(13):
-                for lanes in ((512, 1024, 1536) if form in (2, 8, 9, 10, 12) else (0,)):
+            for form, lanes, sync in [(f, ln, y) for f in range(13)
+                                      for ln in ((512, 1024, 1536) if f in (2, 8, 9, 10, 12) else (0,))
+                                      for y in ((0, 1) if f in (10, 11, 12) else (0,))]:
                     lib.pm_hip_debug_dfa_lds(form)
                     lib.pm_hip_debug_dfa_shape(lanes)
+                    lib.pm_hip_debug_dfa_sync(sync)
                     a = torch.zeros(size, dtype=torch.int32, device="cuda")
                     h = torch.zeros(size, dtype=torch.int16, device="cuda")
                     c = torch.zeros(2, dtype=torch.int64, device="cuda")
@@ -756,13 +758,14 @@ def test_sparse_dfa_kernel_variants_agree(stream):
                     ac.scan_device(dt.data_ptr(), 0, start, size, h.data_ptr(), None, s, out_width=2)
                     ac.scan_device(dt.data_ptr(), 0, start, size, 0, c[1:2].data_ptr(), s)
                     torch.cuda.synchronize()
-                    tag = (size, form, lanes)
+                    tag = (size, form, lanes, sync)
                     assert torch.equal(a, ref[start:start + size]), tag
                     assert torch.equal(h.to(torch.int32) & 0xFFFF, a), tag
                     assert int(c[0].item()) == int(c[1].item()) == int((a != 0).sum().item()), tag
     finally:
         lib.pm_hip_debug_dfa_lds(-1)
         lib.pm_hip_debug_dfa_shape(0)
+        lib.pm_hip_debug_dfa_sync(-1)
         lib.pm_hip_debug_dfa_sparse(-1)
 
 
