@@ -1161,13 +1161,34 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
 constexpr uint32_t DFA_STATE_MASK = 0xFFFFFu;  // must match pm_flatten.h
 constexpr uint32_t DFA_ESC = 4095u;
 
+// The start of the last synchronizing 3-gram in [wlo, lo - 3], or wlo when
+// there is none (DfaDev::gram3: no pattern holds it, so the state after it is
+// the root's over its 3 bytes and a warm-up may start there instead of
+// max_len - 1 bytes back); 16 candidates per round.
+__device__ __forceinline__ int64_t dfa_sync_lo(const uint8_t* __restrict__ text, int64_t lo, int64_t wlo,
+                                               const uint32_t* __restrict__ gram3) {
+    for (int64_t qh = lo - 3; qh >= wlo; qh -= 16) {
+        uint32_t absent = 0;  // bit u: the 3-gram at qh - u is in no pattern
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int64_t q = qh - u;
+            if (q >= wlo) {
+                const uint32_t x = text[q] | (uint32_t)text[q + 1] << 8 | (uint32_t)text[q + 2] << 16;
+                absent |= (~gram3[x >> 5] >> (x & 31) & 1u) << u;
+            }
+        }
+        if (absent) return qh - __builtin_ctz(absent);
+    }
+    return wlo;
+}
+
 template <int OUTW, int CH, int BLK = 16>
 __global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* __restrict__ text, int64_t stream_start,
                                                                 int64_t pos0, int64_t n, void* __restrict__ out,
                                                                 unsigned long long* __restrict__ count,
                                                                 const uint32_t* __restrict__ nxt,
                                                                 const uint32_t* __restrict__ outt, int64_t warm,
-                                                                int64_t seg_len) {
+                                                                int64_t seg_len, const uint32_t* __restrict__ gram3) {
     const int64_t nseg = (n + seg_len - 1) / seg_len;
     const int64_t lanes = (int64_t)gridDim.x * DFA_THREADS;
     uint32_t cnt = 0;
@@ -1181,6 +1202,7 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* _
             hi[k] = sg < nseg ? (lo[k] + seg_len < pos0 + n ? lo[k] + seg_len : pos0 + n) : pos0 + n;
             int64_t wlo = lo[k] - warm;
             if (wlo < stream_start) wlo = stream_start;
+            if (gram3 && sg < nseg) wlo = dfa_sync_lo(text, lo[k], wlo, gram3);
             s[k] = 0;
             if (sg < nseg)
                 for (int64_t i = wlo; i < lo[k]; ++i) s[k] = nxt[(size_t)s[k] * 256 + text[i]] & DFA_STATE_MASK;
@@ -1529,26 +1551,7 @@ void dfa_sparse_lds_kernel(
             if (sg >= nseg) wlo[k] = lo[k];
             s[k] = 0;
             // start the warm-up at the last synchronizing 3-gram before lo
-            // (DfaDev::gram3: no pattern holds it, so the state after it is
-            // the root's over its 3 bytes), 16 candidates per round
-            if (gram3) {
-                bool found = false;
-                for (int64_t qh = lo[k] - 3; !found && qh >= wlo[k]; qh -= 16) {
-                    uint32_t absent = 0;  // bit u: the 3-gram at qh - u is in no pattern
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        const int64_t q = qh - u;
-                        if (q >= wlo[k]) {
-                            const uint32_t x = text[q] | (uint32_t)text[q + 1] << 8 | (uint32_t)text[q + 2] << 16;
-                            absent |= (~gram3[x >> 5] >> (x & 31) & 1u) << u;
-                        }
-                    }
-                    if (absent) {
-                        wlo[k] = qh - __builtin_ctz(absent);
-                        found = true;
-                    }
-                }
-            }
+            if (gram3) wlo[k] = dfa_sync_lo(text, lo[k], wlo[k], gram3);
             wmax = lo[k] - wlo[k] > wmax ? lo[k] - wlo[k] : wmax;
         }
         // (every loop over the chains k is unrolled in the front end: R[k]
@@ -2015,9 +2018,13 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // block instead of once.
 constexpr int SDFA_LANES_PER_CU = 1024;
 static int g_sdfa_lds = -1;
-// warm-ups start at the last synchronizing 3-gram (forms 10 and 12; 0:
-// always max_len - 1 bytes back, timing)
-constexpr int kDfaSyncDefault = 0;
+// Warm-ups start at the last synchronizing 3-gram (dfa_sync_lo; the sparse
+// forms 10-12 and the dense coded kernel; 0: always max_len - 1 bytes back,
+// timing).  Side by side, 1 GiB snort, ms with 0 -> 1 (profiles/r03/
+// dfa_sync_ab.txt): sparse ids lines 8.15 -> 6.61, shipped 5.76 -> 4.63,
+// ASCII 6.62 -> 5.21; sparse count only 6.51 -> 4.92 / 4.61 -> 3.43 /
+// 5.67 -> 4.29; dense ids 19.70 -> 17.32 / 4.02 -> 3.53 / 5.96 -> 4.78.
+constexpr int kDfaSyncDefault = 1;
 static int g_dfa_sync = kDfaSyncDefault;
 static int g_dfa_chains = 0;  // 0: the form's default
 // dense rows or the sparse form for output-coded automata, when a launch
@@ -2035,6 +2042,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
+    const uint32_t* g3 = g_dfa_sync ? t.gram3 : nullptr;  // synchronizing 3-grams (DfaDev::gram3)
     const int lanes_cu = g_dfa_shape_forced || !lds_kernel ? g_dfa_lanes_per_cu : SDFA_LANES_PER_CU;
     const int64_t lanes = (int64_t)num_cu * lanes_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
@@ -2057,7 +2065,6 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         if (wg > cap) wg = cap;
         if (wg < 1) wg = 1;
         const dim3 g2((unsigned)wg), b2(DFA_LDS_THREADS);
-        const uint32_t* g3 = g_dfa_sync ? t.gram3 : nullptr;  // synchronizing 3-grams (DfaDev::gram3)
 #define DL(W, B, K, C)                                                                                               \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, K, C>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
                        t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr)
@@ -2164,10 +2171,10 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     }
     if (t.coded) {
 #define DC(W, C) \
-    hipLaunchKernelGGL((dfa_coded_kernel<W, C>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, t.out, t.warm, seg)
+    hipLaunchKernelGGL((dfa_coded_kernel<W, C>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, t.out, t.warm, seg, g3)
 #define DC32(W, C)                                                                                               \
     hipLaunchKernelGGL((dfa_coded_kernel<W, C, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, \
-                       t.out, t.warm, seg)
+                       t.out, t.warm, seg, g3)
         if (g_dfa_dense_blk == 32 && outw != 0) {
             if (ch == 2) {
                 if (outw == 4) DC32(4, 2); else DC32(2, 2);

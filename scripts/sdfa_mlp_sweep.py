@@ -25,6 +25,7 @@ ap.add_argument("--streams", default="lines")
 ap.add_argument("--forms", default="2,5,6,0")
 ap.add_argument("--lanes", default="512,1024,1536,2048")
 ap.add_argument("--width", type=int, default=4, choices=[0, 2, 4])
+ap.add_argument("--sparse", type=int, default=1, help="1: the sparse form (forms/lanes apply); 0: dense rows")
 ap.add_argument("--sync", default="1", help="warm-ups from synchronizing 3-grams (pm_hip_debug_dfa_sync), e.g. 1,0")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
@@ -34,7 +35,7 @@ d = pm.Dictionary([os.path.join(data, x) for x in DICTS[args.dict]])
 m = pm.HipMatcher("ac")
 m.add_dictionary(d)
 m.compile()
-lib.pm_hip_debug_dfa_sparse(1)
+lib.pm_hip_debug_dfa_sparse(args.sparse)
 n = args.bytes
 w = args.width
 s = torch.cuda.current_stream()
@@ -81,6 +82,6 @@ for st in args.streams.split(","):
         print(f"{st} form {k[0]} lanes/CU {k[1]} sync {k[2]}: {ms:.3f} ms", flush=True)
 lib.pm_hip_debug_dfa_lds(-1)
 lib.pm_hip_debug_dfa_shape(0)
-lib.pm_hip_debug_dfa_sync(1)
+lib.pm_hip_debug_dfa_sync(-1)
 lib.pm_hip_debug_dfa_sparse(-1)
 print(json.dumps(res))

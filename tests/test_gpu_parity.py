@@ -680,7 +680,8 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
     (dfa_coded_kernel) and rows + default-transition records
     (dfa_sparse_kernel, pm_flatten.h) -- give the same u32 / u16 ids and
     counts at every position, at launch sizes from one segment with its
-    warm-up to 64 MiB, and equal the RT kernel."""
+    warm-up to 64 MiB, under both warm-up rules (max_len - 1 bytes back, or
+    from the last synchronizing 3-gram), and equal the RT kernel."""
     torch = _torch()
     lib = pm.load()
     rt, ac = matcher(key, "rt"), matcher(key, "ac")
@@ -699,9 +700,10 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
         for size, start in ((n, 0), (1000, 5000), (100 << 10, 12345), (3 << 20, 1 << 20)):
             start &= ~15
             got = {}
-            for sparse, blk in ((0, 16), (0, 32), (1, 16), (1, 32)):
+            for sparse, blk, sync in [(x, b, y) for x in (0, 1) for b in (16, 32) for y in (0, 1)]:
                 lib.pm_hip_debug_dfa_sparse(sparse)
                 lib.pm_hip_debug_dfa_block(blk)
+                lib.pm_hip_debug_dfa_sync(sync)
                 a = torch.zeros(size, dtype=torch.int32, device="cuda")
                 h = torch.zeros(size, dtype=torch.int16, device="cuda")
                 c = torch.zeros(3, dtype=torch.int64, device="cuda")
@@ -709,9 +711,9 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
                 ac.scan_device(dt.data_ptr(), 0, start, size, h.data_ptr(), c[1:2].data_ptr(), s, out_width=2)
                 ac.scan_device(dt.data_ptr(), 0, start, size, 0, c[2:3].data_ptr(), s)
                 torch.cuda.synchronize()
-                got[(sparse, blk)] = (a, h, c)
-            a0, h0, c0 = got[(0, 16)]
-            for key in ((0, 32), (1, 16), (1, 32)):
+                got[(sparse, blk, sync)] = (a, h, c)
+            a0, h0, c0 = got[(0, 16, 0)]
+            for key in list(got)[1:]:
                 a1, h1, c1 = got[key]
                 assert torch.equal(a0, a1) and torch.equal(h0, h1) and torch.equal(c0, c1), key
             assert torch.equal(a1, ref[start:start + size])
@@ -720,6 +722,7 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
     finally:
         lib.pm_hip_debug_dfa_sparse(-1)
         lib.pm_hip_debug_dfa_block(0)
+        lib.pm_hip_debug_dfa_sync(-1)
 
 
 @pytest.mark.parametrize("stream", ["lines", "ship"])
