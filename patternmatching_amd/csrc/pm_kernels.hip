@@ -2017,6 +2017,7 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // order) at steps whose table load is a register or L2 hit, eight times a
 // block instead of once.
 constexpr int SDFA_LANES_PER_CU = 1024;
+constexpr int DFA_COUNT_LANES_PER_CU = 1024;
 static int g_sdfa_lds = -1;
 // Warm-ups start at the last synchronizing 3-gram (dfa_sync_lo; the sparse
 // forms 10-12 and the dense coded kernel; 0: always max_len - 1 bytes back,
@@ -2043,7 +2044,13 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
     const uint32_t* g3 = g_dfa_sync ? t.gram3 : nullptr;  // synchronizing 3-grams (DfaDev::gram3)
-    const int lanes_cu = g_dfa_shape_forced || !lds_kernel ? g_dfa_lanes_per_cu : SDFA_LANES_PER_CU;
+    // (dense rows, count only: 1,024 lanes per CU once warm-ups start at a
+    // synchronizing 3-gram -- shipped 3.28 -> 2.47 ms, ASCII 4.04 -> 4.10;
+    // profiles/r03/dfa_sync_lanes.txt)
+    const int lanes_cu = g_dfa_shape_forced ? g_dfa_lanes_per_cu
+                         : lds_kernel       ? SDFA_LANES_PER_CU
+                         : t.coded && !sparse && outw == 0 ? DFA_COUNT_LANES_PER_CU
+                                                           : DFA_LANES_PER_CU;
     const int64_t lanes = (int64_t)num_cu * lanes_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
