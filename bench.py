@@ -297,8 +297,17 @@ def main():
 
     import patternmatching_amd as pm
 
-    # one GPU per rank; a rehearsal with more ranks than GPUs (gloo) shares them
-    dev = local % max(1, torch.cuda.device_count())
+    # one GPU per rank.  Under RCCL two ranks on one GPU would hang or fail
+    # inside a collective, so a world larger than the node's GPUs is refused
+    # here, before any collective; a gloo rehearsal (tests) may share one.
+    ngpu = torch.cuda.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if use_dist and backend == "nccl" and (local_world > ngpu or local >= ngpu):
+        print(f"bench.py: {local_world} ranks on this node (LOCAL_RANK {local}) but {ngpu} visible GPU(s); "
+              "RCCL needs one GPU per rank (PM_BENCH_BACKEND=gloo rehearses ranks sharing a GPU)",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
+    dev = local % max(1, ngpu)
     torch.cuda.set_device(dev)
     if use_dist:
         if backend == "nccl":
@@ -307,6 +316,18 @@ def main():
             dist.init_process_group(backend)
         assert dist.get_world_size() == world
     coll = "cuda" if backend == "nccl" else "cpu"  # gloo rehearsals reduce host tensors
+    prop = torch.cuda.get_device_properties(dev)
+    my_dev = {"ordinal": dev, "pci_bus_id": "%04x:%02x:%02x.0" % (prop.pci_domain_id, prop.pci_bus_id,
+                                                                  prop.pci_device_id),
+              "uuid": str(getattr(prop, "uuid", "")), "name": prop.name}
+    devices = [my_dev]
+    if use_dist:
+        devices = [None] * world
+        dist.all_gather_object(devices, my_dev)
+        if backend == "nccl" and len({d["pci_bus_id"] for d in devices}) != world:
+            if rank == 0:
+                print(f"bench.py: ranks share GPUs under RCCL: {devices}", file=sys.stderr, flush=True)
+            sys.exit(3)
 
     def all_reduce(t, op):
         if not use_dist:
@@ -406,7 +427,11 @@ def main():
     per_rank = all_gather([float(rank), elapsed_mine, kernel_ms_mine])
     stats = all_reduce(torch.tensor([elapsed_mine, kernel_ms_mine], dtype=torch.float64, device="cuda"),
                        dist.ReduceOp.MAX)
+    torch.cuda.synchronize()
+    t_cnt = time.perf_counter()
     matches = all_reduce(count.clone(), dist.ReduceOp.SUM)  # RCCL over xGMI: the match-count reduction
+    torch.cuda.synchronize()
+    count_ar_ms = (time.perf_counter() - t_cnt) * 1e3
 
     # after the timed region: all-matches (patterns ending at each position,
     # i.e. the suffix-chain length of each id), the per-pattern histogram
@@ -483,7 +508,7 @@ def main():
 
     # the default run's extra lines: count-only on the same stream, and the
     # deep lines stream through the auto kind
-    count_only = deep = None
+    count_only = deep = configs = None
     if extras_on(args):
         ksteps = min(args.steps, 10)
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -509,6 +534,7 @@ def main():
         d_ms = all_reduce(torch.tensor([d_ms], dtype=torch.float64, device="cuda"), dist.ReduceOp.MAX).item()
         d_matches = all_reduce(dcnt.clone(), dist.ReduceOp.SUM).item() // dsteps
         ach = n * 5 / (d_ms * 1e-3) / 1e9
+        dtr = load_traffic(f"{args.dict}-lines-{n}-dense-auto")
         deep = {"kernel": "auto kind (RT, or after a deep RT launch the faster AC-DFA form by timed trials)",
                 "picked": CAND_NAME.get(d_held, str(d_held)), "stream": "lines", "mode": "dense",
                 "steps": dsteps, "kernel_ms": round(d_ms, 4),
@@ -517,9 +543,13 @@ def main():
                 "data": "synthetic deep-match stream: the dictionary's own patterns drawn at random (splitmix64 "
                         "per 1 KiB block), '\\n' after each, generated in HBM (DESIGN.md §5)",
                 "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": n * 5},
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": n * 5,
+                             "traffic": dtr["traffic_bytes"] if dtr else None,
+                             "traffic_source": dtr["source"] if dtr else None},
                 "cpu_baseline": cpu.get("deep") if cpu else None}
         ma.free()
+        del ma
+        configs = other_configs(args, pm, lib, world, all_reduce, dist, text=text, out=out)
 
     if rank == 0:
         last_kernel = CAND_NAME.get(held, "RT") if held > 0 else "RT" if args.kernel == "rt" else "AC"
@@ -565,8 +595,10 @@ def main():
                 "layout": args.layout,
             },
             "world_size": world,
-            "per_rank": [{"rank": int(r[0]), "gbps": round(g, 3), "kernel_ms": round(r[2], 4)}
+            "per_rank": [{"rank": int(r[0]), "gbps": round(g, 3), "kernel_ms": round(r[2], 4),
+                          "device": devices[int(r[0])]}
                          for r, g in zip(per_rank, rates)],
+            "match_count_all_reduce_ms": round(count_ar_ms, 3) if use_dist else None,
             "rank_spread": round(max(rates) / min(rates), 4),
             "matches_per_sec": round(total_matches / elapsed, 1),
             "matches_per_step": total_matches // max(1, args.steps),
@@ -588,10 +620,76 @@ def main():
             "cpu_baseline": cpu["main"] if cpu else None,
             **({"count_only": count_only} if count_only else {}),
             **({"deep": deep} if deep else {}),
+            **({"configs": configs} if extras_on(args) else {}),
         }
         print(json.dumps(res), flush=True)
     if use_dist:
         dist.destroy_process_group()
+
+
+def other_configs(args, pm, lib, world, all_reduce, dist, text, out):
+    """The other BASELINE.json configs on the same kernels, per rank, timed
+    like the headline (max over ranks): C2 (et.dict, 64 MiB ASCII, dense
+    u32 ids), C5 (snort + et merged, 4 GiB ASCII: four 1 GiB launches per
+    step, dense u32) and the merged dictionary on the deep lines stream
+    through the auto kind.  The 1 GiB text and id buffers of the headline
+    are reused where they are large enough."""
+    import torch
+    res = {}
+    stream = torch.cuda.current_stream()
+    rank = int(os.environ.get("RANK", "0"))
+
+    def run(name, dict_key, kind, stream_kind, nbytes, steps):
+        d = pm.Dictionary([os.path.join(DATA, x) for x in DICTS[dict_key]])
+        m = pm.HipMatcher(kind)
+        m.add_dictionary(d)
+        m.compile()
+        t = text if nbytes <= text.numel() - 64 else torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+        o = out if nbytes <= out.numel() else torch.empty(nbytes, dtype=torch.int32, device="cuda")
+        if stream_kind == "lines":
+            m.gen_lines_device(t.data_ptr(), nbytes + 64, args.seed + rank, stream.cuda_stream)
+        elif lib.pm_hip_gen_stream_device(t.data_ptr(), 0, nbytes + 64, args.seed + rank, 0, stream.cuda_stream):
+            raise RuntimeError(lib.pm_hip_last_error().decode())
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+        def step():
+            m.scan_device(t.data_ptr(), 0, 0, nbytes, o.data_ptr(), cnt.data_ptr(), stream.cuda_stream)
+        held = m.hold_choice(0)
+        for _ in range(12):
+            if held != -1:
+                break
+            step()
+            torch.cuda.synchronize()
+            held = m.hold_choice(0)
+        step()
+        torch.cuda.synchronize()
+        held = m.hold_choice(steps + 1)
+        cnt.zero_()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for e0, e1 in evs:
+            e0.record(stream)
+            step()
+            e1.record(stream)
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+        ms = all_reduce(torch.tensor([ms], dtype=torch.float64, device="cuda"), dist.ReduceOp.MAX).item()
+        matches = all_reduce(cnt.clone(), dist.ReduceOp.SUM).item() // steps
+        ach = nbytes * 5 / (ms * 1e-3) / 1e9
+        res[name] = {"dict": dict_key, "stream": stream_kind, "bytes_per_gpu": nbytes, "mode": "dense",
+                     "kernel": kind + ("" if kind == "rt" else f" (held: {CAND_NAME.get(held, str(held))})"),
+                     "steps": steps, "kernel_ms": round(ms, 4),
+                     "stream_gbps": round(world * nbytes / (ms * 1e-3) / 1e9, 2),
+                     "matches_per_step": int(matches),
+                     "table_bytes": int(m.table_bytes),
+                     "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes * 5}}
+        m.free()
+        del t, o
+
+    run("C2_et_64MiB", "et", "rt", "ascii", 64 << 20, 20)
+    run("C5_merged_4GiB", "merged", "rt", "ascii", 4 << 30, 5)
+    run("merged_lines_auto", "merged", "auto", "lines", min(args.bytes, 1 << 30), 5)
+    return res
 
 
 def load_traffic(workload_key):

@@ -116,6 +116,18 @@ int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, un
  * to make (rt kind, or a single DFA form), -1 while the pick is still being
  * measured (launch more, synchronize, and ask again). */
 int pm_hip_hold_choice(void* obj, int launches);
+/* Before a scan_device launch is captured into a HIP graph (hipStreamBeginCapture,
+ * torch.cuda.graph): allocates the scratch captured launches of the rt / auto
+ * kinds use (the reverse-trie kernel's spill regions, sized for a launch of
+ * any length: 512 MiB on 256 CUs), since nothing may be allocated while a
+ * stream captures.  Without it a captured scan_device returns -5 and
+ * launches nothing.  Direct launches allocate their own scratch per stream
+ * (pm_hip_scratch_bytes).  0 on success. */
+int pm_hip_prepare_capture(void* obj);
+/* Device scratch the object holds beside its tables (pm_hip_table_bytes):
+ * the capture scratch, the per-stream scratch of direct scan_device
+ * launches and the read_block pipeline's staging.  Bytes. */
+size_t pm_hip_scratch_bytes(void* obj);
 /* Compiled-image cache: compile() keeps the flattened tables of each
  * dictionary in DIR (pm-<kind>-<hash>.img, keyed by the patterns in add order)
  * and reuses them; without a call here, $PM_IMAGE_CACHE names the directory

@@ -1656,6 +1656,210 @@ void dfa_sparse_lds_kernel(
     }
 }
 
+// The sparse form with decoupled lanes (round 4).  In the lock-step kernels
+// above every lane steps one position per wave step, so a wave step waits for
+// its slowest lane's chain of dependent loads: a record block, then at a slot
+// miss the fallback row's word.  On the lines stream 74% of wave steps wait
+// for two dependent loads and 99% for at least one (1.73 load latencies per
+// wave step; scripts/sdfa_wave_model.cpp).  Here each lane walks its own
+// segment at its own pace: a position whose step needs a global load (a row
+// word, a record block, an escaped id) makes the lane stop for this wave
+// step; every lane's load is issued at the END of the wave step, and the
+// next wave step starts by waiting for all of them, so a wave step costs at
+// most one load latency and a lane that needs two dependent loads spends two
+// wave steps on that position while the others go on.  A lane does at most
+// K positions per wave step.  Modelled: 2,914 wave steps per 4 KiB segment
+// at K = 2 against 4,213 x 1.73 load latencies in lock step.
+// Lanes are at different positions, so their ids cannot sit in registers
+// indexed by position: each lane stages SB coded ids in LDS (a slot per
+// position, ds_write_b32) and, when its SB positions are done, stops for the
+// wave step and writes them out as whole 16-B vectors (SB = 32: one 128-B
+// line).  Text: a 16-B window per lane in registers and the next one loaded
+// when the lane enters a window (at least 16 / K wave steps ahead).
+template <int OUTW, int K, int KR, int SB, int THREADS>
+__global__ __launch_bounds__(THREADS) void dfa_sparse_dyn_kernel(
+    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
+    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
+    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
+    constexpr int SBW = OUTW ? SB : 4;
+    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_ids[THREADS * SBW];
+    if (KR) {
+        const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_rows);
+        for (uint32_t k = threadIdx.x; k < nr * 64u; k += THREADS) dst[k] = src[k];
+        __syncthreads();
+    }
+    enum : uint32_t { REQ_NONE = 0, REQ_BLOCK = 1, REQ_WORD = 2, REQ_ESC = 3 };
+    const int64_t nseg = (n + seg_len - 1) / seg_len;
+    const int64_t sg = (int64_t)blockIdx.x * THREADS + threadIdx.x;  // at most one segment per lane (host)
+    bool live = sg < nseg;
+    const int64_t lo = live ? pos0 + sg * seg_len : 0;
+    const int64_t hi = live ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : 0;
+    int64_t p = lo - warm < stream_start ? stream_start : lo - warm;
+    if (!live) p = 0;
+    if (live && gram3) p = dfa_sync_lo(text, lo, p, gram3);
+    int64_t tw = p & ~(int64_t)15;  // the text window [tw, tw + 16) in A, the next one in B
+    const tu32x4 zero4 = {0u, 0u, 0u, 0u};
+    tu32x4 A = live ? *reinterpret_cast<const tu32x4*>(text + tw) : zero4;
+    tu32x4 B = live && tw + 16 < hi ? *reinterpret_cast<const tu32x4*>(text + tw + 16) : zero4;
+    tu32x4 R[4] = {zero4, zero4, zero4, zero4};  // the aligned block of 8 record units holding state s
+    uint32_t s = 0, cb = 0xFFFFFFFFu, cnt = 0;
+    uint32_t req = REQ_NONE, nb = 0, escj = 0, V = 0;
+    const uint32_t* waddr = outt;  // a REQ_WORD / REQ_ESC load's address
+    bool treq = false;             // load the next text window at the end of the wave step
+    bool fl = false;               // a staged block is complete: write it out at the end of the wave step
+    uint32_t fj = 0, fc = 0;       // its first slot (position - lo) and its positions
+    uint32_t* const stage = s_ids + threadIdx.x * SBW;
+    // staging slot of position offset j: 16-B chunks rotated by the lane, so
+    // lanes at the same slot hit different banks
+    auto slot = [&](uint32_t j) __attribute__((always_inline)) {
+        return ((((j >> 2) + threadIdx.x) & (SB / 4 - 1)) << 2) | (j & 3u);
+    };
+    auto staged = [&](uint32_t j) __attribute__((always_inline)) {
+        // the block of position offset j is complete once its last slot is
+        // staged (or the segment ends)
+        if ((j & (SB - 1)) == SB - 1 || lo + j + 1 == hi) {
+            fl = true;
+            fj = j & ~(uint32_t)(SB - 1);
+            fc = j - fj + 1;
+        }
+    };
+    // position p's transition word v: the state, the id, the count
+    auto complete = [&](uint32_t v) __attribute__((always_inline)) {
+        s = v & DFA_STATE_MASK;
+        const uint32_t code = v >> 20;
+        if (p >= lo) {
+            const uint32_t j = (uint32_t)(p - lo);
+            cnt += code != 0u;
+            if (OUTW) {
+                if (code == DFA_ESC) {
+                    req = REQ_ESC;
+                    escj = j;
+                    waddr = outt + s;
+                } else {
+                    stage[slot(j)] = code;
+                    staged(j);
+                }
+            }
+        }
+        ++p;
+    };
+    for (;;) {
+        // ---- the loads of the last wave step have landed: resolve them
+        if (req == REQ_BLOCK) cb = nb;  // the position is retried below
+        if (req == REQ_WORD) {
+            req = REQ_NONE;
+            complete(V);
+        } else if (req == REQ_ESC) {
+            req = REQ_NONE;
+            stage[slot(escj)] = V;
+            staged(escj);
+        } else {
+            req = REQ_NONE;
+        }
+        // ---- up to K positions per lane, no global load among them
+#pragma unroll
+        for (int it = 0; it < K; ++it) {
+            if (live && req == REQ_NONE && !fl && p < hi) {
+                if (p >= tw + 16) {  // the next window (loaded at least one wave step ago)
+                    A = B;
+                    tw += 16;
+                    treq = tw + 16 < hi;
+                }
+                const uint32_t off = (uint32_t)(p - tw);
+                const uint32_t w01 = (off & 4u) ? A.y : A.x, w23 = (off & 4u) ? A.w : A.z;
+                const uint32_t c = (((off & 8u) ? w23 : w01) >> (8 * (off & 3u))) & 0xFFu;
+                if (s < F) {
+                    if (KR && s < (uint32_t)KR) {
+                        complete(s_rows[s * 256u + c]);
+                    } else {
+                        req = REQ_WORD;
+                        waddr = reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
+                    }
+                } else {
+                    const uint32_t rec = s - F, b = rec >> 3;
+                    if (b != cb) {
+                        req = REQ_BLOCK;  // this position again once the block is in
+                        nb = b;
+                    } else {
+                        // the 8-B unit form (pm_pack_sparse8): one unit {y, x0 | w << 9},
+                        // or two {y, x | 1 << 31}, {z, w} in the same block
+                        const uint32_t e = rec & 7u, key = c | 0x100u;
+                        const tu32x4 q = (e & 4u) ? ((e & 2u) ? R[3] : R[2]) : ((e & 2u) ? R[1] : R[0]);
+                        const uint32_t e2 = ((e >> 1) + 1u) & 3u;
+                        const tu32x4 q2 = (e2 & 2u) ? ((e2 & 1u) ? R[3] : R[2]) : ((e2 & 1u) ? R[1] : R[0]);
+                        const uint32_t y = (e & 1u) ? q.z : q.x, x = (e & 1u) ? q.w : q.y;
+                        uint32_t w = (x >> 9) & 0x3FFFFFu, hitv = y;
+                        bool hit = (x & 0x1FFu) == key;
+                        if (x >> 31) {
+                            const uint32_t z = (e & 1u) ? q2.x : q.z;
+                            if (!hit && ((x >> 16) & 0x1FFu) == key) {
+                                hit = true;
+                                hitv = z;
+                            }
+                            w = (e & 1u) ? q2.y : q.w;
+                        }
+                        if (hit) {
+                            complete(hitv);
+                        } else if (KR && w < (uint32_t)KR) {
+                            complete(s_rows[w * 256u + c]);
+                        } else {
+                            req = REQ_WORD;
+                            waddr = reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
+                        }
+                    }
+                }
+            }
+        }
+        // ---- end of the wave step: write out complete staged blocks, issue
+        // every lane's load (waited for at the top of the next wave step)
+        if (OUTW && fl) {
+            const int64_t o = lo - pos0 + fj;
+            if (fc == (uint32_t)SB) {
+                tu32x4 v[SB / 4];
+#pragma unroll
+                for (int q = 0; q < SB / 4; ++q)
+                    v[q] = *reinterpret_cast<const tu32x4*>(stage + ((((uint32_t)q + threadIdx.x) & (SB / 4 - 1)) << 2));
+                if (OUTW == 4) {
+                    tu32x4* dst = reinterpret_cast<tu32x4*>(reinterpret_cast<uint32_t*>(out) + o);
+#pragma unroll
+                    for (int q = 0; q < SB / 4; ++q) dst[q] = v[q];
+                } else {
+                    tu32x4* dst = reinterpret_cast<tu32x4*>(reinterpret_cast<uint16_t*>(out) + o);
+#pragma unroll
+                    for (int q = 0; q < SB / 8; ++q)
+                        dst[q] = tu32x4{v[2 * q].x | v[2 * q].y << 16, v[2 * q].z | v[2 * q].w << 16,
+                                        v[2 * q + 1].x | v[2 * q + 1].y << 16, v[2 * q + 1].z | v[2 * q + 1].w << 16};
+                }
+            } else {  // the segment's last, partial block
+                for (uint32_t j = 0; j < fc; ++j) put_id<OUTW>(out, o + j, stage[slot(fj + j)]);
+            }
+            fl = false;
+        }
+        if (req == REQ_BLOCK) {
+            const tu32x4* pb = reinterpret_cast<const tu32x4*>(base + F * 1024u + nb * 64u);
+            R[0] = pb[0];
+            R[1] = pb[1];
+            R[2] = pb[2];
+            R[3] = pb[3];
+        } else if (req != REQ_NONE) {
+            V = *waddr;
+        }
+        if (treq) {
+            B = *reinterpret_cast<const tu32x4*>(text + tw + 16);
+            treq = false;
+        }
+        live = p < hi || req != REQ_NONE;
+        if (!__ballot(live)) break;  // wave-uniform
+    }
+    if (count) {
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
+    }
+}
+
 // Accuracy of one id stream against a reference one (Core/src/measure.c:
 // 174-190 with is_pattern_suffix, PatternsTree.c:485-494), one position per
 // lane-element: equal -> success; algo on real's parent chain -> partial;
@@ -1865,7 +2069,17 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
     const int64_t blocks = rt_blocks(n, num_cu);
     RtDev t = t0;
     t.spill_stride = rt_spill_stride(n, blocks);
-    if (blocks * RT_WAVES * t.spill_stride > t.spill_cap) return hipErrorInvalidValue;  // caller sizes it (pm_rt_spill_items)
+    // The caller sizes the scratch (pm_rt_spill_items) with the cap in force
+    // then; a cap raised since (pm_rt_set_spill_cap, timing sweeps) must not
+    // turn a scratch sized before it into a failed launch: the stride is
+    // clamped to what the scratch holds, whole chunks, at least one (the
+    // kernel resolves a full region and goes on, so any stride of >= one
+    // chunk is exact).
+    const int64_t fit = t.spill_cap / (blocks * RT_WAVES) / RT_CHUNK * RT_CHUNK;
+    if (t.spill_stride > fit) {
+        if (fit < RT_CHUNK) return hipErrorInvalidValue;  // scratch smaller than one chunk per wave
+        t.spill_stride = fit;
+    }
     const dim3 g((unsigned)blocks), b(RT_THREADS);
 #define RT_LAUNCH(VV)                                                                                             \
     do {                                                                                                          \
@@ -2063,6 +2277,32 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), b(DFA_THREADS);
+    if (lds_kernel && sdfa_lds >= 13 && t.sbase8) {
+        // decoupled lanes (dfa_sparse_dyn_kernel): one segment per lane
+        // (seg above gives nseg <= lanes), DYN_THREADS lanes per workgroup
+        constexpr int DT = 256;
+        const dim3 g3d((unsigned)std::max<int64_t>(1, (nseg + DT - 1) / DT)), b3d(DT);
+#define DY(W, KK, R, S)                                                                                          \
+    hipLaunchKernelGGL((dfa_sparse_dyn_kernel<W, KK, R, S, DT>), g3d, b3d, 0, s, text, stream_start, pos0, n, out, \
+                       count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
+#define DYW(KK, R, S)                                      \
+    do {                                                   \
+        if (outw == 4) DY(4, KK, R, S);                    \
+        else if (outw == 2) DY(2, KK, R, S);               \
+        else DY(0, KK, R, S);                              \
+    } while (0)
+        switch (sdfa_lds) {
+            case 14: DYW(1, 0, 32); break;
+            case 15: DYW(3, 0, 32); break;
+            case 16: DYW(2, 16, 32); break;
+            case 17: DYW(2, 0, 16); break;
+            case 18: DYW(4, 0, 32); break;
+            default: DYW(2, 0, 32); break;  // 13
+        }
+#undef DY
+#undef DYW
+        return hipGetLastError();
+    }
     if (lds_kernel) {
         // one workgroup of DFA_LDS_THREADS lanes per CU, persistent over
         // the segments (the LDS rows are staged once per workgroup)
@@ -2217,7 +2457,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 12 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 18 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }

@@ -187,6 +187,21 @@ void free_pick(AutoPick& a) {
     a = AutoPick();
 }
 
+// The measurement resources of a kind that picks per launch (KIND_AUTO /
+// KIND_AC): made when the object or slot is set up, never at a launch, so a
+// launch under stream capture (which may not allocate) finds them.
+void init_pick(AutoPick& a, int kind, bool has_sparse) {
+    if (a.ev || (kind != KIND_AUTO && kind != KIND_AC)) return;
+    if (kind == KIND_AC) a.chosen = has_sparse ? CAND_SPARSE : CAND_DENSE;  // no RT image
+    PM_CHECK(hipMalloc(&a.d_spill, sizeof(unsigned long long)));
+    PM_CHECK(hipHostMalloc(&a.h_spill, sizeof(unsigned long long), hipHostMallocDefault));
+    PM_CHECK(hipEventCreateWithFlags(&a.ev, hipEventDisableTiming));
+    for (int c = 0; c < NCAND; ++c) {
+        PM_CHECK(hipEventCreate(&a.t0[c]));
+        PM_CHECK(hipEventCreate(&a.t1[c]));
+    }
+}
+
 void* dalloc_copy(PmHip* o, const void* src, size_t bytes) {
     void* p = nullptr;
     PM_CHECK(hipMalloc(&p, bytes ? bytes : 16));
@@ -275,6 +290,7 @@ void ensure_slot(PmHip* o, PipeSlot& q, size_t positions) {
         PM_CHECK(hipEventCreate(&q.ev0));
         PM_CHECK(hipEventCreate(&q.ev1));
     }
+    init_pick(q.pick, o->kind, o->dfa.sbase != nullptr);
     if (positions <= q.cap) return;
     free_slot(q);
     const size_t cap = std::max(positions, (size_t)1 << 16);
@@ -284,6 +300,7 @@ void ensure_slot(PmHip* o, PipeSlot& q, size_t positions) {
     PM_CHECK(hipHostMalloc(&q.h_stage, stage_bytes, hipHostMallocDefault));
     PM_CHECK(hipHostMalloc(&q.h_res, cap * sizeof(uint32_t), hipHostMallocDefault));
     ensure_spill(o, q.spill, q.spill_cap, (int64_t)cap);
+    init_pick(q.pick, o->kind, o->dfa.sbase != nullptr);
     q.cap = cap;
 }
 
@@ -403,20 +420,12 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
     // its untimed pick launches, pm_hip_hold_choice).  The read_block
     // pipeline has synchronized the slot already, so there it lands at the
     // next call.  Under stream capture nothing is measured (no events, no
-    // copies): the current choice runs.
-    if (!ap.ev) {
-        if (o->kind == KIND_AC) ap.chosen = o->dfa.sbase ? CAND_SPARSE : CAND_DENSE;  // no RT image
-        PM_CHECK(hipMalloc(&ap.d_spill, sizeof(unsigned long long)));
-        PM_CHECK(hipHostMalloc(&ap.h_spill, sizeof(unsigned long long), hipHostMallocDefault));
-        PM_CHECK(hipEventCreateWithFlags(&ap.ev, hipEventDisableTiming));
-        for (int c = 0; c < NCAND; ++c) {
-            PM_CHECK(hipEventCreate(&ap.t0[c]));
-            PM_CHECK(hipEventCreate(&ap.t1[c]));
-        }
-    }
+    // copies, nothing allocated -- the pick's resources are made with the
+    // object, init_pick): the current choice runs.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
         return launch_cand(o, ap, ap.chosen, text, stream_start, pos0, n, out, outw, count, s, t);
+    init_pick(ap, o->kind, o->dfa.sbase != nullptr);
     resolve_pick(o, ap);
     if (ap.hold > 0) {  // hold the chosen kernel
         --ap.hold;
@@ -668,7 +677,7 @@ void pm_hip_compile(void* obj) {
         }
     }
     o->hist.init(o->max_len);
-    ensure_spill(o, o->spill, o->spill_cap, INT64_MAX);  // the bound for any scan_device launch
+    init_pick(o->pick, o->kind, o->dfa.sbase != nullptr);
     o->d_parent = (const uint32_t*)dalloc_copy(o, im.par.parent.data(), im.par.parent.size() * 4);
     o->d_depth = (const uint32_t*)dalloc_copy(o, im.par.depth.data(), im.par.depth.size() * 4);
     o->parent = std::move(im.par.parent);
@@ -787,6 +796,14 @@ static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         e = hipStreamIsCapturing(s, &cs);
         StreamSpill* sp = e == hipSuccess && cs == hipStreamCaptureStatusNone ? stream_spill(o, s, n) : nullptr;
+        if (e == hipSuccess && cs != hipStreamCaptureStatusNone && !o->spill &&
+            (o->kind == KIND_RT || o->kind == KIND_AUTO)) {
+            // nothing launched: the capture stays valid for the caller to end
+            std::snprintf(g_err, sizeof(g_err),
+                          "scan_device under stream capture needs pm_hip_prepare_capture(obj) first (the RT "
+                          "kernel's scratch cannot be allocated while a stream captures)");
+            return -5;
+        }
         if (e == hipSuccess)
             e = launch(o, d_text, stream_start, pos0, n, d_out, outw, d_count, s, sp ? sp->buf : o->spill,
                        sp ? sp->cap : o->spill_cap, o->pick);
@@ -846,6 +863,24 @@ int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, un
         return -3;
     }
     return 0;
+}
+
+int pm_hip_prepare_capture(void* obj) {
+    PmHip* o = as(obj);
+    if (!o->compiled) { std::snprintf(g_err, sizeof(g_err), "not compiled"); return -1; }
+    if (hipSetDevice(o->device) != hipSuccess) { std::snprintf(g_err, sizeof(g_err), "set device"); return -3; }
+    ensure_spill(o, o->spill, o->spill_cap, INT64_MAX);  // the bound for any scan_device launch
+    init_pick(o->pick, o->kind, o->dfa.sbase != nullptr);
+    return 0;
+}
+
+size_t pm_hip_scratch_bytes(void* obj) {
+    PmHip* o = as(obj);
+    size_t b = (size_t)o->spill_cap * 8;
+    for (const StreamSpill& x : o->sspill) b += (size_t)x.cap * 8;
+    for (const PipeSlot& q : o->slot)
+        b += (size_t)q.spill_cap * 8 + (q.d_stage ? q.cap * sizeof(uint32_t) + q.cap + o->max_len + 64 : 0);
+    return b;
 }
 
 int pm_hip_hold_choice(void* obj, int launches) {

@@ -229,6 +229,16 @@ class HipMatcher:
         0 = nothing to pick; -1 = still measuring)."""
         return self.lib.pm_hip_hold_choice(self.obj, launches)
 
+    def prepare_capture(self):
+        """pm_hip_prepare_capture: the scratch captured scan_device launches
+        need, allocated before any stream capture begins."""
+        if self.lib.pm_hip_prepare_capture(self.obj) != 0:
+            raise RuntimeError(self.lib.pm_hip_last_error().decode())
+
+    @property
+    def scratch_bytes(self):
+        return self.lib.pm_hip_scratch_bytes(self.obj)
+
     def parent_gid(self, gid):
         return self.lib.pm_hip_parent_gid(self.obj, gid)
 

@@ -88,6 +88,8 @@ def gen_tree(manifest):
 
 
 def main():
+    if not os.path.exists(DRIVER):
+        sys.exit("build the reference driver first: make -C oracle ref")
     if sys.argv[1:] == ["tree"]:  # only section (6), into the existing manifest
         path = os.path.join(HERE, "manifest.json")
         with open(path) as f:
@@ -96,8 +98,6 @@ def main():
         with open(path, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
         return
-    if not os.path.exists(DRIVER):
-        sys.exit("build the reference driver first: make -C oracle ref")
     os.makedirs(DATA, exist_ok=True)
     for name in ("et.dict", "snort.dict"):
         shutil.copyfile(os.path.join(REF, "Dictionaries", name), os.path.join(DATA, name))

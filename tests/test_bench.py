@@ -83,6 +83,20 @@ def test_world_size_mismatch_is_an_error():
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
 
 
+def test_more_ranks_than_gpus_is_refused_under_rccl():
+    """Under RCCL a rank per GPU: a node world larger than the visible GPUs
+    exits 3 with a message before any collective (instead of two ranks
+    sharing a GPU and hanging in one); no rendezvous is attempted."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--no-cpu"]
+    e = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", LOCAL_WORLD_SIZE="4096",
+             MASTER_ADDR="127.0.0.1", MASTER_PORT="1")
+    for k in ("PM_BENCH_REHEARSE", "PM_BENCH_BACKEND"):
+        e.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=e, cwd=REPO)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "one GPU per rank" in r.stderr
+
+
 def _run(extra, env=None):
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--bytes", str(16 << 20), "--steps", "2", "--warmup", "1",
            "--no-cpu"] + extra

@@ -19,6 +19,14 @@ KIND_OF = {"rt": pm.KIND_RT, "ac": pm.KIND_AC, "auto": pm.KIND_AUTO}
 _m = {}
 
 
+def fresh_matcher(key, kind):
+    """A new compiled object (never launched), not the cached one."""
+    m = pm.HipMatcher(kind)
+    m.add_dictionary(pm.Dictionary(dict_paths(key)))
+    m.compile()
+    return m
+
+
 def matcher(key, kind):
     if (key, kind) not in _m:
         d = pm.Dictionary(dict_paths(key))
@@ -727,9 +735,10 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
 
 @pytest.mark.parametrize("stream", ["lines", "ship"])
 def test_sparse_dfa_kernel_variants_agree(stream):
-    """Every kernel of the sparse form (pm_hip_debug_dfa_lds 0-12: plain, LDS
+    """Every kernel of the sparse form (pm_hip_debug_dfa_lds 0-18: plain, LDS
     rows, register record blocks, two segments per lane, 16-position blocks,
-    capped registers)
+    capped registers, decoupled lanes with 1-4 positions per wave step, LDS
+    rows and 16-position staging)
     at 512 / 1024 / 1536 lanes per CU gives the RT
     kernel's u32 / u16 ids and the same count, at sizes from one warm-up
     segment to 32 MiB (snort)."""
@@ -748,9 +757,9 @@ def test_sparse_dfa_kernel_variants_agree(stream):
     lib.pm_hip_debug_dfa_sparse(1)
     try:
         for size, start in ((n, 0), (777, 4096), (100 << 10, 12345 & ~15), (5 << 20, 3 << 20)):
-            for form, lanes, sync in [(f, ln, y) for f in range(13)
-                                      for ln in ((512, 1024, 1536) if f in (2, 8, 9, 10, 12) else (0,))
-                                      for y in ((0, 1) if f in (10, 11, 12) else (0,))]:
+            for form, lanes, sync in [(f, ln, y) for f in range(19)
+                                      for ln in ((512, 1024, 1536) if f in (2, 8, 9, 10, 12, 13) else (0,))
+                                      for y in ((0, 1) if f in (10, 11, 12, 13, 16) else (0,))]:
                     lib.pm_hip_debug_dfa_lds(form)
                     lib.pm_hip_debug_dfa_shape(lanes)
                     lib.pm_hip_debug_dfa_sync(sync)
@@ -768,6 +777,56 @@ def test_sparse_dfa_kernel_variants_agree(stream):
     finally:
         lib.pm_hip_debug_dfa_lds(-1)
         lib.pm_hip_debug_dfa_shape(0)
+        lib.pm_hip_debug_dfa_sync(-1)
+        lib.pm_hip_debug_dfa_sparse(-1)
+
+
+@pytest.mark.parametrize("stream", ["lines", "ship"])
+def test_dfa_warmups_stop_at_stream_start(stream):
+    """Bytes before stream_start are not the stream: the DFA warm-ups (from
+    max_len - 1 bytes back, or from the last synchronizing 3-gram,
+    dfa_sync_lo) must not look at them.  The bytes before stream_start are
+    pattern-dense text of another seed, stream_start is not aligned, and the
+    first positions lie within max_len of it; every DFA form (dense rows;
+    sparse plain / record blocks / 8-B units / LDS rows) under both warm-up
+    rules gives the RT kernel's u32 / u16 ids and count."""
+    torch = _torch()
+    lib = pm.load()
+    rt, ac = matcher("snort", "rt"), matcher("snort", "ac")
+    n = 4 << 20
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    if stream == "lines":
+        rt.gen_lines_device(dt.data_ptr(), n + 64, 13, s)
+    else:
+        dt.copy_(torch.from_numpy(np.tile(SHIP, (n + 64) // len(SHIP) + 1)[: n + 64]).cuda())
+    garbage = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    rt.gen_lines_device(garbage.data_ptr(), n + 64, 99, s)
+    try:
+        for stream_start, pos0, size in ((4099, 4112, 1 << 20), (77, 80, 3000), (1000, 1040, 2 << 20),
+                                         (12345, 12352 + 4096, 1 << 20)):
+            buf = garbage.clone()
+            buf[stream_start:] = dt[: n + 64 - stream_start]
+            ref = torch.empty(size, dtype=torch.int32, device="cuda")
+            rt.scan_device(buf.data_ptr(), stream_start, pos0, size, ref.data_ptr(), None, s)
+            forms = [(0, -1, y) for y in (0, 1)] + [(1, f, y) for f in (0, 2, 10, 12, 13, 16) for y in (0, 1)]
+            for sparse, lds, sync in forms:
+                lib.pm_hip_debug_dfa_sparse(sparse)
+                lib.pm_hip_debug_dfa_lds(lds)
+                lib.pm_hip_debug_dfa_sync(sync)
+                a = torch.zeros(size, dtype=torch.int32, device="cuda")
+                h = torch.zeros(size, dtype=torch.int16, device="cuda")
+                c = torch.zeros(1, dtype=torch.int64, device="cuda")
+                ac.scan_device(buf.data_ptr(), stream_start, pos0, size, a.data_ptr(), None, s)
+                ac.scan_device(buf.data_ptr(), stream_start, pos0, size, h.data_ptr(), None, s, out_width=2)
+                ac.scan_device(buf.data_ptr(), stream_start, pos0, size, 0, c.data_ptr(), s)
+                torch.cuda.synchronize()
+                tag = (stream_start, pos0, sparse, lds, sync)
+                assert torch.equal(a, ref), tag
+                assert torch.equal(h.to(torch.int32) & 0xFFFF, a), tag
+                assert int(c.item()) == int((a != 0).sum().item()), tag
+    finally:
+        lib.pm_hip_debug_dfa_lds(-1)
         lib.pm_hip_debug_dfa_sync(-1)
         lib.pm_hip_debug_dfa_sparse(-1)
 
@@ -986,6 +1045,7 @@ def test_auto_scan_device_under_graph_capture():
     text = _tiled_ship(n)
     dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
     m = matcher("et", "auto")
+    m.prepare_capture()
     s = torch.cuda.Stream()
     want = torch.empty(n, dtype=torch.int32, device="cuda")
     got = torch.zeros(n, dtype=torch.int32, device="cuda")
@@ -1003,6 +1063,74 @@ def test_auto_scan_device_under_graph_capture():
         torch.cuda.synchronize()
         assert torch.equal(got, want)
         assert int(cnt.item()) == int((want != 0).sum().item())
+
+
+@pytest.mark.parametrize("kind", ["auto", "ac", "rt"])
+def test_first_scan_device_inside_graph_capture(kind):
+    """The very first scan_device of a new object inside a capture: with
+    pm_hip_prepare_capture before it the launch is captured and a replay
+    gives the RT kernel's eager ids; without it (rt / auto, whose scratch
+    cannot be allocated under capture) scan_device fails with an error,
+    launches nothing, and the capture ends cleanly.  Nothing is allocated
+    under capture either way (pm_plugin.hip init_pick)."""
+    import torch
+    n = 4 << 20
+    dt = torch.from_numpy(np.concatenate([_tiled_ship(n), np.zeros(64, np.uint8)])).cuda()
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    matcher("et", "rt").scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None,
+                                    torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    if kind != "ac":
+        bare = fresh_matcher("et", kind)
+        got = torch.zeros(n, dtype=torch.int32, device="cuda")
+        g = torch.cuda.CUDAGraph()
+        with pytest.raises(RuntimeError, match="prepare_capture"):
+            with torch.cuda.graph(g, stream=s):
+                bare.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
+        torch.cuda.synchronize()
+    m = fresh_matcher("et", kind)
+    m.prepare_capture()
+    assert m.scratch_bytes >= (0 if kind == "ac" else 1 << 20)
+    got = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), cnt.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        cnt.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(got, want)
+        assert int(cnt.item()) == int((want != 0).sum().item())
+
+
+def test_spill_cap_raised_after_prepare():
+    """A spill cap raised after the capture scratch was sized (timing
+    sweeps) clamps the captured launch's regions to the scratch instead of
+    failing it; the ids stay exact."""
+    import torch
+    n = 128 << 20  # 32 chunks per wave: past the default 16-chunk regions
+    dt = torch.from_numpy(np.concatenate([_tiled_ship(n), np.zeros(64, np.uint8)])).cuda()
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    matcher("et", "ac").scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None,
+                                    torch.cuda.current_stream().cuda_stream)
+    lib = pm.load()
+    m = fresh_matcher("et", "rt")
+    m.prepare_capture()
+    s = torch.cuda.Stream()
+    got = torch.zeros(n, dtype=torch.int32, device="cuda")
+    try:
+        lib.pm_hip_debug_spill_cap(64)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        lib.pm_hip_debug_spill_cap(0)
+    assert torch.equal(got, want)
 
 
 @pytest.mark.parametrize("stream", ["ship", "lines"])
