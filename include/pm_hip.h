@@ -229,6 +229,10 @@ void pm_hip_debug_spill_cap(int chunks);
 /* Timing sweeps only: at most b workgroups per reverse-trie launch (0 = one
  * per CU). */
 void pm_hip_debug_rt_blocks(int b);
+/* Timing only: the read_block host path's breakdown since the last call --
+ * out5 = {staging s, enqueue s, wait s, result copy / map s, calls} -- then
+ * reset and turn the accounting on (on != 0) or off. */
+void pm_hip_debug_host_profile(int on, double* out5);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

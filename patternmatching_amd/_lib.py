@@ -135,6 +135,7 @@ SIGNATURES = {
     "pm_hip_hbm_peak_gbs": (ctypes.c_double, []),
     "pm_hip_hold_choice": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "pm_hip_prepare_capture": (ctypes.c_int, [c_vp]),
+    "pm_hip_debug_host_profile": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "pm_hip_scratch_bytes": (ctypes.c_size_t, [c_vp]),
     "pm_flat_host_scan": (ctypes.c_int, [c_vp, c_u8p, ctypes.c_size_t, c_u32p, ctypes.c_int]),
 }

@@ -1165,18 +1165,27 @@ constexpr uint32_t DFA_ESC = 4095u;
 // there is none (DfaDev::gram3: no pattern holds it, so the state after it is
 // the root's over its 3 bytes and a warm-up may start there instead of
 // max_len - 1 bytes back); 16 candidates per round.
+// Every load of a round is issued before any is used (the 18 bytes, then
+// the 16 set words): two load latencies per round.  (With a branch per
+// candidate the compiler had waited for each byte in turn: 48 latencies.)
 __device__ __forceinline__ int64_t dfa_sync_lo(const uint8_t* __restrict__ text, int64_t lo, int64_t wlo,
                                                const uint32_t* __restrict__ gram3) {
     for (int64_t qh = lo - 3; qh >= wlo; qh -= 16) {
+        uint32_t b[18];  // bytes qh - 15 .. qh + 2 (any before wlo read as text[wlo], then masked)
+#pragma unroll
+        for (int u = 0; u < 18; ++u) {
+            const int64_t q = qh - 15 + u;
+            b[u] = text[q < wlo ? wlo : q];
+        }
+        uint32_t g[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {  // the 3-gram at qh - u
+            const uint32_t x = b[15 - u] | b[16 - u] << 8 | b[17 - u] << 16;
+            g[u] = gram3[x >> 5] >> (x & 31);
+        }
         uint32_t absent = 0;  // bit u: the 3-gram at qh - u is in no pattern
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int64_t q = qh - u;
-            if (q >= wlo) {
-                const uint32_t x = text[q] | (uint32_t)text[q + 1] << 8 | (uint32_t)text[q + 2] << 16;
-                absent |= (~gram3[x >> 5] >> (x & 31) & 1u) << u;
-            }
-        }
+        for (int u = 0; u < 16; ++u) absent |= (uint32_t)(qh - u >= wlo && !(g[u] & 1u)) << u;
         if (absent) return qh - __builtin_ctz(absent);
     }
     return wlo;
@@ -1512,13 +1521,19 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
 
 // WPE: the waves per SIMD the register allocation must allow (0: the
 // compiler's choice); each more resident workgroup is 512 more chains per CU
-template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0, int RB = 16, int TB = 1>
+// TX (u32 ids, 32-position blocks, one chain per lane): the block's ids go
+// out through LDS, transposed so that every store instruction writes eight
+// whole 128-B lines (eight lanes per line) instead of a 16-B piece of 64
+// lines; 1 = non-temporal stores (the lines need no L2 room), 2 = plain.
+template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0, int RB = 16, int TB = 1, int TX = 0>
 __global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void dfa_sparse_lds_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
     const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
+    constexpr bool kTX = TX && OUTW == 4 && BLK == 32 && CH == 1;
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 1];
+    __shared__ __attribute__((aligned(16))) uint4 s_tx[kTX ? DFA_LDS_THREADS * 8 : 1];
     if (KR) {
         const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
         const uint4* src = reinterpret_cast<const uint4*>(base);
@@ -1537,8 +1552,11 @@ void dfa_sparse_lds_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) R[k][e] = make_uint4(0u, 0u, 0u, 0u);
     }
-    // CH segments per lane in lock step (sg0 + k * lanes), their loads in flight together
-    for (int64_t sg0 = (int64_t)blockIdx.x * DFA_LDS_THREADS + threadIdx.x; sg0 < nseg; sg0 += CH * lanes) {
+    // CH segments per lane in lock step (sg0 + k * lanes), their loads in flight together.
+    // (kTX: every loop is wave-uniform -- lanes without a segment or past
+    // their last block still take part in the id exchange)
+    for (int64_t sg0 = (int64_t)blockIdx.x * DFA_LDS_THREADS + threadIdx.x;
+         kTX ? __ballot(sg0 < nseg) != 0 : sg0 < nseg; sg0 += CH * lanes) {
         int64_t lo[CH], hi[CH], wlo[CH];
         uint32_t s[CH];
         int64_t wmax = 0;
@@ -1591,10 +1609,10 @@ void dfa_sparse_lds_kernel(
                     }
                 }
             }
-            if (!anyt[0]) break;
+            if (kTX ? !__ballot(anyt[0]) : !anyt[0]) break;
             unroll_for<0, TB>([&](auto tc) {
             constexpr int tt = decltype(tc)::value;
-            if (tt > 0 && !anyt[tt]) return;
+            if (tt > 0 && (kTX ? !__ballot(anyt[tt]) : !anyt[tt])) return;
             const int64_t b = b0 + tt;
             const bool(&act)[CH] = actt[tt];
             const uint32_t(&W)[CH][NW] = WT[tt];
@@ -1613,6 +1631,38 @@ void dfa_sparse_lds_kernel(
             }
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
+                if (kTX) {
+                    // every lane takes part in the exchange; only active
+                    // chains' lines are stored
+                    uint32_t r[BLK];
+#pragma unroll
+                    for (int j = 0; j < BLK; ++j)
+                        r[j] = (vw[k][j] >> 20) == DFA_ESC && act[k] ? outt[vw[k][j] & DFA_STATE_MASK] : vw[k][j] >> 20;
+                    const int lane = threadIdx.x & 63;
+                    tu32x4* const W = reinterpret_cast<tu32x4*>(s_tx) + (threadIdx.x >> 6) * 512;  // this wave's 64 lines
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)  // 16-B chunk q of my line, XOR-swizzled over the banks
+                        W[lane * 8 + (q ^ (lane & 7))] = tu32x4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
+                    __builtin_amdgcn_wave_barrier();
+                    const uint64_t am = __ballot(act[k]);
+                    const int64_t sgl = sg0 - lane;  // the wave's first chain
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const int c = 8 * t + (lane >> 3);  // chain whose line this lane stores a chunk of
+                        const tu32x4 v = W[c * 8 + ((lane & 7) ^ (c & 7))];
+                        if ((am >> c) & 1u) {
+                            const int64_t ic = pos0 + (sgl + c) * seg_len + BLK * b;
+                            tu32x4* o = reinterpret_cast<tu32x4*>(reinterpret_cast<uint32_t*>(out) + (ic - pos0)) + (lane & 7);
+                            if (TX == 1) __builtin_nontemporal_store(v, o);
+                            else *o = v;
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    if (act[k])
+#pragma unroll
+                        for (int j = 0; j < BLK; ++j) cnt += r[j] != 0u;
+                    continue;
+                }
                 if (!act[k]) continue;
                 uint32_t r[BLK];
                 // (count only: an escape code is a nonzero id, no lookup)
@@ -1674,8 +1724,12 @@ void dfa_sparse_lds_kernel(
 // indexed by position: each lane stages SB coded ids in LDS (a slot per
 // position, ds_write_b32) and, when its SB positions are done, stops for the
 // wave step and writes them out as whole 16-B vectors (SB = 32: one 128-B
-// line).  Text: a 16-B window per lane in registers and the next one loaded
-// when the lane enters a window (at least 16 / K wave steps ahead).
+// line).  Text: a 32-B window per lane in registers (A, B), refilled only at
+// wave-synchronous points every TSYNC wave steps: a lane advances at most
+// K + 1 positions per wave step, so between two refills it stays inside the
+// window, and only one wave step in TSYNC waits for text from HBM (a refill
+// at each lane's own time put an HBM miss into nearly every wave step: a wave
+// step waits for every load of the one before).
 template <int OUTW, int K, int KR, int SB, int THREADS>
 __global__ __launch_bounds__(THREADS) void dfa_sparse_dyn_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
@@ -1700,15 +1754,16 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_dyn_kernel(
     int64_t p = lo - warm < stream_start ? stream_start : lo - warm;
     if (!live) p = 0;
     if (live && gram3) p = dfa_sync_lo(text, lo, p, gram3);
-    int64_t tw = p & ~(int64_t)15;  // the text window [tw, tw + 16) in A, the next one in B
+    int64_t tw = p & ~(int64_t)15;  // the text window [tw, tw + 32): A, B
     const tu32x4 zero4 = {0u, 0u, 0u, 0u};
     tu32x4 A = live ? *reinterpret_cast<const tu32x4*>(text + tw) : zero4;
     tu32x4 B = live && tw + 16 < hi ? *reinterpret_cast<const tu32x4*>(text + tw + 16) : zero4;
+    constexpr int TSYNC = 16 / (K + 1);  // wave steps between text refills
+    int tphase = 0;                      // wave-uniform
     tu32x4 R[4] = {zero4, zero4, zero4, zero4};  // the aligned block of 8 record units holding state s
     uint32_t s = 0, cb = 0xFFFFFFFFu, cnt = 0;
     uint32_t req = REQ_NONE, nb = 0, escj = 0, V = 0;
     const uint32_t* waddr = outt;  // a REQ_WORD / REQ_ESC load's address
-    bool treq = false;             // load the next text window at the end of the wave step
     bool fl = false;               // a staged block is complete: write it out at the end of the wave step
     uint32_t fj = 0, fc = 0;       // its first slot (position - lo) and its positions
     uint32_t* const stage = s_ids + threadIdx.x * SBW;
@@ -1763,13 +1818,9 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_dyn_kernel(
 #pragma unroll
         for (int it = 0; it < K; ++it) {
             if (live && req == REQ_NONE && !fl && p < hi) {
-                if (p >= tw + 16) {  // the next window (loaded at least one wave step ago)
-                    A = B;
-                    tw += 16;
-                    treq = tw + 16 < hi;
-                }
-                const uint32_t off = (uint32_t)(p - tw);
-                const uint32_t w01 = (off & 4u) ? A.y : A.x, w23 = (off & 4u) ? A.w : A.z;
+                const uint32_t off = (uint32_t)(p - tw);  // < 32 (TSYNC)
+                const tu32x4 H = (off & 16u) ? B : A;
+                const uint32_t w01 = (off & 4u) ? H.y : H.x, w23 = (off & 4u) ? H.w : H.z;
                 const uint32_t c = (((off & 8u) ? w23 : w01) >> (8 * (off & 3u))) & 0xFFu;
                 if (s < F) {
                     if (KR && s < (uint32_t)KR) {
@@ -1847,9 +1898,13 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_dyn_kernel(
         } else if (req != REQ_NONE) {
             V = *waddr;
         }
-        if (treq) {
-            B = *reinterpret_cast<const tu32x4*>(text + tw + 16);
-            treq = false;
+        if (++tphase == TSYNC) {  // wave-uniform: the text refill point
+            tphase = 0;
+            if (live && p >= tw + 16) {
+                A = B;
+                tw += 16;
+                if (tw + 16 < hi) B = *reinterpret_cast<const tu32x4*>(text + tw + 16);
+            }
         }
         live = p < hi || req != REQ_NONE;
         if (!__ballot(live)) break;  // wave-uniform
@@ -2277,27 +2332,27 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), b(DFA_THREADS);
-    if (lds_kernel && sdfa_lds >= 13 && t.sbase8) {
+    if (lds_kernel && sdfa_lds >= 13 && sdfa_lds <= 18 && t.sbase8) {
         // decoupled lanes (dfa_sparse_dyn_kernel): one segment per lane
         // (seg above gives nseg <= lanes), DYN_THREADS lanes per workgroup
-        constexpr int DT = 256;
+        const int DT = sdfa_lds >= 16 ? 1024 : 256;
         const dim3 g3d((unsigned)std::max<int64_t>(1, (nseg + DT - 1) / DT)), b3d(DT);
-#define DY(W, KK, R, S)                                                                                          \
-    hipLaunchKernelGGL((dfa_sparse_dyn_kernel<W, KK, R, S, DT>), g3d, b3d, 0, s, text, stream_start, pos0, n, out, \
+#define DY(W, KK, R, S, T)                                                                                         \
+    hipLaunchKernelGGL((dfa_sparse_dyn_kernel<W, KK, R, S, T>), g3d, b3d, 0, s, text, stream_start, pos0, n, out, \
                        count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-#define DYW(KK, R, S)                                      \
+#define DYW(KK, R, S, T)                                   \
     do {                                                   \
-        if (outw == 4) DY(4, KK, R, S);                    \
-        else if (outw == 2) DY(2, KK, R, S);               \
-        else DY(0, KK, R, S);                              \
+        if (outw == 4) DY(4, KK, R, S, T);                 \
+        else if (outw == 2) DY(2, KK, R, S, T);            \
+        else DY(0, KK, R, S, T);                           \
     } while (0)
         switch (sdfa_lds) {
-            case 14: DYW(1, 0, 32); break;
-            case 15: DYW(3, 0, 32); break;
-            case 16: DYW(2, 16, 32); break;
-            case 17: DYW(2, 0, 16); break;
-            case 18: DYW(4, 0, 32); break;
-            default: DYW(2, 0, 32); break;  // 13
+            case 14: DYW(1, 0, 32, 256); break;
+            case 15: DYW(3, 0, 32, 256); break;
+            case 16: DYW(2, 64, 16, 1024); break;  // one workgroup per CU: 64 rows + 16-position staging
+            case 17: DYW(1, 64, 16, 1024); break;
+            case 18: DYW(3, 64, 16, 1024); break;
+            default: DYW(2, 0, 32, 256); break;  // 13
         }
 #undef DY
 #undef DYW
@@ -2324,6 +2379,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #define DL8K(W, K)                                                                                                    \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, K, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
                        count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
+#define DL8X(K, X)                                                                                                 \
+    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, K, 1, 0, 8, 2, X>), g2, b2, 0, s, text, stream_start, pos0, n, \
+                       out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
 #define DLW(W, B, E)                                                                                                 \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, 0, 1, E>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
                        t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr)
@@ -2368,6 +2426,19 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                     if (outw == 4) DL8K(4, 64); else if (outw == 2) DL8K(2, 64); else DL8K(0, 64);
                 }
                 break;
+            case 19:  // (10) with the ids through LDS as whole lines, non-temporal (u32 ids)
+            case 20:  // the same, plain stores
+            case 21:  // (12) with non-temporal whole-line ids
+                if (!t.sbase8 || outw != 4) {
+                    if (outw == 4) DL8T(4); else if (outw == 2) DL8T(2); else DL8T(0);
+                } else if (sdfa_lds == 19) {
+                    DL8X(0, 1);
+                } else if (sdfa_lds == 20) {
+                    DL8X(0, 2);
+                } else {
+                    DL8X(64, 1);
+                }
+                break;
             case 8:  // the same, registers capped for 6 waves per SIMD (three workgroups per CU)
                 if (outw == 4) DLW(4, 16, 6); else if (outw == 2) DLW(2, 16, 6); else DLW(0, 16, 8);
                 break;
@@ -2380,6 +2451,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #undef DL8
 #undef DL8T
 #undef DL8K
+#undef DL8X
         return hipGetLastError();
     }
     if (sparse) {
@@ -2457,7 +2529,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 18 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 21 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }

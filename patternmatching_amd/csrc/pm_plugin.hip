@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -304,6 +305,17 @@ void ensure_slot(PmHip* o, PipeSlot& q, size_t positions) {
     q.cap = cap;
 }
 
+// Zero-copy small read_block calls (PM_HOST_ZC, a bit mask; timing A/B):
+// 1 = the kernel writes its results straight into the pinned result buffer,
+// 2 = it reads the pinned staging buffer instead of a device copy.
+int host_zero_copy() {
+    static const int z = [] {
+        const char* e = std::getenv("PM_HOST_ZC");
+        return e ? (int)std::strtol(e, nullptr, 10) & 3 : 0;
+    }();
+    return z;
+}
+
 // Host threads for the copy/map work around the pipeline (PM_HOST_THREADS,
 // default min(8, hardware threads)).
 unsigned host_threads() {
@@ -473,6 +485,15 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
 // dictionary) come back as u16 gids (half the PCIe bytes) for the host
 // threads to map: +12% (RT) / +28% (AC).  Gids for the caller stay u32 and
 // direct: widening u16 on the host measured 2-5% slower.  Rates: DESIGN.md §5.
+// Host-path breakdown (pm_hip_debug_host_profile): seconds spent staging
+// the input, enqueueing the copies and the launch, waiting for the slot,
+// and copying / mapping the results; calls.
+double g_hprof[5] = {0, 0, 0, 0, 0};
+bool g_hprof_on = false;
+inline double hp_now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pattern_id_t* out_ids) {
     if (!o->compiled) {
         std::fprintf(stderr, "pm_hip: read before compile\n");
@@ -483,8 +504,18 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
     const size_t pipe = out_gid ? PIPE_GID_POSITIONS : PIPE_ID_POSITIONS;
     const bool narrow = !out_gid && o->gids.index_of_gid.size() <= 65536;  // u16 gids over PCIe
     o->last_out_width = narrow ? 2 : 4;
+    double t_mark = g_hprof_on ? hp_now() : 0.0;
+    auto lap = [&](int k) {
+        if (!g_hprof_on) return;
+        const double t = hp_now();
+        g_hprof[k] += t - t_mark;
+        t_mark = t;
+    };
+    if (g_hprof_on) g_hprof[4] += 1;
     auto finish = [&](PipeSlot& q) {
+        lap(1);
         PM_CHECK(hipStreamSynchronize(q.stream));
+        lap(2);
         float ms = 0.f;
         PM_CHECK(hipEventElapsedTime(&ms, q.ev0, q.ev1));
         o->dev_seconds += ms * 1e-3;
@@ -505,6 +536,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             std::memcpy(out_gid + q.off, q.h_res, q.m * sizeof(uint32_t));
         }
         q.busy = false;
+        lap(3);
     };
     size_t done = 0;
     for (int k = 0; done < n; ++k) {
@@ -524,10 +556,14 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             std::memcpy(st + from_hist, buf, done);
         }
         q.staged = m <= PIPE_SMALL_POSITIONS;
+        // small blocks, zero-copy (host_zero_copy()): the kernel reads the
+        // pinned staging (2) / writes the pinned results (1) over the link
+        const bool zc_in = q.staged && (host_zero_copy() & 2), zc_out = q.staged && (host_zero_copy() & 1);
         if (q.staged) {  // [context | bytes | 16 zero bytes] in one DMA from pinned memory
             std::memcpy(q.h_stage + ctx, buf + done, m);
             std::memset(q.h_stage + ctx + m, 0, 16);
-            PM_CHECK(hipMemcpyAsync(q.d_stage, q.h_stage, ctx + m + 16, hipMemcpyHostToDevice, q.stream));
+            lap(0);
+            if (!zc_in) PM_CHECK(hipMemcpyAsync(q.d_stage, q.h_stage, ctx + m + 16, hipMemcpyHostToDevice, q.stream));
         } else {
             std::memset(q.h_stage + ctx, 0, 16);
             if (ctx) PM_CHECK(hipMemcpyAsync(q.d_stage, q.h_stage, ctx, hipMemcpyHostToDevice, q.stream));
@@ -535,12 +571,14 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
         }
         PM_CHECK(hipEventRecord(q.ev0, q.stream));
-        PM_CHECK(launch(o, q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.d_res, narrow ? 2 : 4, nullptr,
-                        q.stream, q.spill, q.spill_cap, q.pick));
+        PM_CHECK(launch(o, zc_in ? q.h_stage : q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m,
+                        zc_out ? q.h_res : q.d_res, narrow ? 2 : 4, nullptr, q.stream, q.spill, q.spill_cap, q.pick));
         o->last_kernel = q.pick.last ? q.pick.last : o->kind;
         o->last_form = q.pick.last_form;
         PM_CHECK(hipEventRecord(q.ev1, q.stream));
-        if (narrow)
+        if (zc_out)
+            ;  // the results are in h_res once the stream is done
+        else if (narrow)
             PM_CHECK(hipMemcpyAsync(q.h_res, q.d_res, m * sizeof(uint16_t), hipMemcpyDeviceToHost, q.stream));
         else
             PM_CHECK(hipMemcpyAsync(out_gid && !q.staged ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
@@ -684,6 +722,13 @@ void pm_hip_compile(void* obj) {
     o->id_of_gid.assign(o->gids.index_of_gid.size(), PM_NULL_PATTERN_ID);
     for (size_t g = 1; g < o->gids.index_of_gid.size(); ++g) o->id_of_gid[g] = o->ids[o->gids.index_of_gid[g]];
     o->compiled = true;
+}
+
+void pm_hip_debug_host_profile(int on, double* out5) {
+    if (out5)
+        for (int k = 0; k < 5; ++k) out5[k] = g_hprof[k];
+    for (double& x : g_hprof) x = 0.0;
+    g_hprof_on = on != 0;
 }
 
 int pm_hip_read_block_gid(void* obj, const uint8_t* buf, size_t n, uint32_t* out_gid) {
