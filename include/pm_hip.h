@@ -216,7 +216,11 @@ void pm_hip_debug_dfa_variant(int v);
  * segments per lane, 7 / 8 = (2) with 16-position blocks (8: registers
  * capped for 6 waves per SIMD), 9 = (2) over 8-B record units, 10 = (9)
  * with two blocks' text per load, 11 / 12 = (10) with 32 / 64 rows in LDS;
- * -1 = the product choice (12 for ids, 10 for count only). */
+ * 22 / 23 / 24 = (12) without HBM id lines / escape lookups / id stores
+ * (timing ablations: wrong ids); 25 / 26 = ids staged in LDS and stored as
+ * whole lines (plain / non-temporal), 27 = 25 with 1024-lane workgroups and
+ * 16 rows in LDS, 28 = 27 with 4-unit (32-B) record blocks;
+ * -1 = the product choice (28 for u32 ids, 12 for u16, 10 for count only). */
 void pm_hip_debug_dfa_lds(int v);
 /* Timing experiments only: 0 = every warm-up of the sparse form's product
  * kernels starts max_len - 1 bytes back; 1 = at the last synchronizing

@@ -437,7 +437,7 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
     uint64_t u = 0;  // next free unit
     for (uint32_t v = F; v < S; ++v) {
         const bool two = (rec[(size_t)(v - F) * 4] & 0x1000000u) != 0;
-        if (two && (u & 7) == 7) ++u;  // keep both units in one 64-B block
+        if (two && (u & 3) == 3) ++u;  // keep both units in one aligned 32-B (so also 64-B) block
         nid[v] = F + (uint32_t)u;
         u += two ? 2 : 1;
         if (F + u > PM_DFA_STATE_MASK + 1) return false;

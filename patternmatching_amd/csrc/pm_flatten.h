@@ -156,8 +156,8 @@ PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap&
 //   zero or one slot (75% of snort's records): one unit {y, x0 | w << 9},
 //     x0 = c0 | 0x100 (0: no slot), w = the fallback row;
 //   two slots: two units {y, x | 1 << 31}, {z, w} (x as in the 16-B
-//     form), never straddling an aligned 64-B block of 8 units (a padding
-//     unit before it when it would).
+//     form), never straddling an aligned 32-B block of 4 units (so neither
+//     a 64-B block of 8; a padding unit before it when it would).
 // Every coded word's target is renumbered; out8 is indexed by the new ids
 // (padding ids 0).  A walk along a pattern's unary run reads twice as many
 // states per line as with 16-B records.  False when the new ids do not fit

@@ -1477,29 +1477,36 @@ __device__ __forceinline__ uint4 pick4(const uint4 (&R)[4], uint32_t k) {
 // 8-B unit form (pm_pack_sparse8), 8 units per block: a one-slot record is
 // one unit {y, x0 | w << 9}, a two-slot record two {y, x | 1 << 31}, {z, w}
 // in the same block.
-template <int KR, int RB = 16>
+// BU (RB = 8): units per register block -- 8 (64 B, four 16-B loads) or 4
+// (32 B, two loads; pm_pack_sparse8 keeps a two-unit record inside an
+// aligned 32-B block)
+template <int KR, int RB = 16, int BU = 8>
 __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ base, uint32_t F,
                                                   const uint32_t* __restrict__ s_rows, uint32_t s, uint32_t c,
                                                   uint32_t& cb, uint4 (&R)[4]) {
+    static_assert(BU == 8 || (BU == 4 && RB == 8), "4-unit blocks are 8-B units");
     const bool isrow = s < F;
-    const uint32_t rec = s - F, b = rec >> (RB == 8 ? 3 : 2);
+    const uint32_t rec = s - F, b = rec >> (RB == 8 ? (BU == 8 ? 3 : 2) : 2);
     uint32_t rv = 0;
     if (isrow) {
         if (KR && s < (uint32_t)KR) rv = s_rows[s * 256u + c];
         else rv = *reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
     } else if (b != cb) {
-        const uint4* p = reinterpret_cast<const uint4*>(base + F * 1024u + b * 64u);
+        const uint4* p = reinterpret_cast<const uint4*>(base + F * 1024u + b * (BU == 8 ? 64u : 32u));
         R[0] = p[0];
         R[1] = p[1];
-        R[2] = p[2];
-        R[3] = p[3];
+        if (BU == 8) {
+            R[2] = p[2];
+            R[3] = p[3];
+        }
         cb = b;
     }
     if (isrow) return rv;
     const uint32_t key = c | 0x100u;
     if (RB == 8) {
-        const uint32_t e = rec & 7u;
-        const uint4 q = pick4(R, e >> 1), q2 = pick4(R, ((e >> 1) + 1u) & 3u);
+        const uint32_t e = rec & (BU - 1u);
+        const uint4 q = BU == 8 ? pick4(R, e >> 1) : ((e & 2u) ? R[1] : R[0]);
+        const uint4 q2 = BU == 8 ? pick4(R, ((e >> 1) + 1u) & 3u) : ((e & 2u) ? R[0] : R[1]);
         const uint32_t y = (e & 1u) ? q.z : q.x, x = (e & 1u) ? q.w : q.y;
         if ((x & 0x1FFu) == key) return y;
         uint32_t w = (x >> 9) & 0x3FFFFFu;
@@ -1521,19 +1528,16 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
 
 // WPE: the waves per SIMD the register allocation must allow (0: the
 // compiler's choice); each more resident workgroup is 512 more chains per CU
-// TX (u32 ids, 32-position blocks, one chain per lane): the block's ids go
-// out through LDS, transposed so that every store instruction writes eight
-// whole 128-B lines (eight lanes per line) instead of a 16-B piece of 64
-// lines; 1 = non-temporal stores (the lines need no L2 room), 2 = plain.
+// TX: timing ablations of the id output (u32 ids; wrong ids): 3 = every
+// block's ids to one line per lane (stays in L2), 4 = no escape lookups,
+// 5 = no id stores (profiles/r04/dyn/store_escape_ablations.txt).
 template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0, int RB = 16, int TB = 1, int TX = 0>
 __global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void dfa_sparse_lds_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
     const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
-    constexpr bool kTX = TX && OUTW == 4 && BLK == 32 && CH == 1;
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 1];
-    __shared__ __attribute__((aligned(16))) uint4 s_tx[kTX ? DFA_LDS_THREADS * 8 : 1];
     if (KR) {
         const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
         const uint4* src = reinterpret_cast<const uint4*>(base);
@@ -1552,11 +1556,8 @@ void dfa_sparse_lds_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) R[k][e] = make_uint4(0u, 0u, 0u, 0u);
     }
-    // CH segments per lane in lock step (sg0 + k * lanes), their loads in flight together.
-    // (kTX: every loop is wave-uniform -- lanes without a segment or past
-    // their last block still take part in the id exchange)
-    for (int64_t sg0 = (int64_t)blockIdx.x * DFA_LDS_THREADS + threadIdx.x;
-         kTX ? __ballot(sg0 < nseg) != 0 : sg0 < nseg; sg0 += CH * lanes) {
+    // CH segments per lane in lock step (sg0 + k * lanes), their loads in flight together
+    for (int64_t sg0 = (int64_t)blockIdx.x * DFA_LDS_THREADS + threadIdx.x; sg0 < nseg; sg0 += CH * lanes) {
         int64_t lo[CH], hi[CH], wlo[CH];
         uint32_t s[CH];
         int64_t wmax = 0;
@@ -1609,10 +1610,10 @@ void dfa_sparse_lds_kernel(
                     }
                 }
             }
-            if (kTX ? !__ballot(anyt[0]) : !anyt[0]) break;
+            if (!anyt[0]) break;
             unroll_for<0, TB>([&](auto tc) {
             constexpr int tt = decltype(tc)::value;
-            if (tt > 0 && (kTX ? !__ballot(anyt[tt]) : !anyt[tt])) return;
+            if (tt > 0 && !anyt[tt]) return;
             const int64_t b = b0 + tt;
             const bool(&act)[CH] = actt[tt];
             const uint32_t(&W)[CH][NW] = WT[tt];
@@ -1631,47 +1632,25 @@ void dfa_sparse_lds_kernel(
             }
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
-                if (kTX) {
-                    // every lane takes part in the exchange; only active
-                    // chains' lines are stored
-                    uint32_t r[BLK];
-#pragma unroll
-                    for (int j = 0; j < BLK; ++j)
-                        r[j] = (vw[k][j] >> 20) == DFA_ESC && act[k] ? outt[vw[k][j] & DFA_STATE_MASK] : vw[k][j] >> 20;
-                    const int lane = threadIdx.x & 63;
-                    tu32x4* const W = reinterpret_cast<tu32x4*>(s_tx) + (threadIdx.x >> 6) * 512;  // this wave's 64 lines
-#pragma unroll
-                    for (int q = 0; q < 8; ++q)  // 16-B chunk q of my line, XOR-swizzled over the banks
-                        W[lane * 8 + (q ^ (lane & 7))] = tu32x4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
-                    __builtin_amdgcn_wave_barrier();
-                    const uint64_t am = __ballot(act[k]);
-                    const int64_t sgl = sg0 - lane;  // the wave's first chain
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        const int c = 8 * t + (lane >> 3);  // chain whose line this lane stores a chunk of
-                        const tu32x4 v = W[c * 8 + ((lane & 7) ^ (c & 7))];
-                        if ((am >> c) & 1u) {
-                            const int64_t ic = pos0 + (sgl + c) * seg_len + BLK * b;
-                            tu32x4* o = reinterpret_cast<tu32x4*>(reinterpret_cast<uint32_t*>(out) + (ic - pos0)) + (lane & 7);
-                            if (TX == 1) __builtin_nontemporal_store(v, o);
-                            else *o = v;
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    if (act[k])
-#pragma unroll
-                        for (int j = 0; j < BLK; ++j) cnt += r[j] != 0u;
-                    continue;
-                }
                 if (!act[k]) continue;
                 uint32_t r[BLK];
-                // (count only: an escape code is a nonzero id, no lookup)
+                // (count only: an escape code is a nonzero id, no lookup;
+                // TX = 4, timing ablation: no escape lookups either)
 #pragma unroll
                 for (int j = 0; j < BLK; ++j)
-                    r[j] = OUTW && (vw[k][j] >> 20) == DFA_ESC ? outt[vw[k][j] & DFA_STATE_MASK] : vw[k][j] >> 20;
+                    r[j] = OUTW && TX != 4 && (vw[k][j] >> 20) == DFA_ESC ? outt[vw[k][j] & DFA_STATE_MASK]
+                                                                         : vw[k][j] >> 20;
                 const int64_t i = lo[k] + BLK * b;
+                if (TX == 5) {  // timing ablation: the ids computed (escapes too), not stored
+#pragma unroll
+                    for (int j = 0; j < BLK; ++j) cnt += r[j];
+                    continue;
+                }
                 if (OUTW == 4) {
-                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
+                    // (TX = 3, timing ablation: every block's ids to the
+                    // same line per lane, which stays in L2 -- wrong ids)
+                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) +
+                                                        (TX == 3 ? (int64_t)threadIdx.x * BLK : i - pos0));
 #pragma unroll
                     for (int q = 0; q < BLK / 4; ++q)
                         o[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
@@ -1706,38 +1685,35 @@ void dfa_sparse_lds_kernel(
     }
 }
 
-// The sparse form with decoupled lanes (round 4).  In the lock-step kernels
-// above every lane steps one position per wave step, so a wave step waits for
-// its slowest lane's chain of dependent loads: a record block, then at a slot
-// miss the fallback row's word.  On the lines stream 74% of wave steps wait
-// for two dependent loads and 99% for at least one (1.73 load latencies per
-// wave step; scripts/sdfa_wave_model.cpp).  Here each lane walks its own
-// segment at its own pace: a position whose step needs a global load (a row
-// word, a record block, an escaped id) makes the lane stop for this wave
-// step; every lane's load is issued at the END of the wave step, and the
-// next wave step starts by waiting for all of them, so a wave step costs at
-// most one load latency and a lane that needs two dependent loads spends two
-// wave steps on that position while the others go on.  A lane does at most
-// K positions per wave step.  Modelled: 2,914 wave steps per 4 KiB segment
-// at K = 2 against 4,213 x 1.73 load latencies in lock step.
-// Lanes are at different positions, so their ids cannot sit in registers
-// indexed by position: each lane stages SB coded ids in LDS (a slot per
-// position, ds_write_b32) and, when its SB positions are done, stops for the
-// wave step and writes them out as whole 16-B vectors (SB = 32: one 128-B
-// line).  Text: a 32-B window per lane in registers (A, B), refilled only at
-// wave-synchronous points every TSYNC wave steps: a lane advances at most
-// K + 1 positions per wave step, so between two refills it stays inside the
-// window, and only one wave step in TSYNC waits for text from HBM (a refill
-// at each lane's own time put an HBM miss into nearly every wave step: a wave
-// step waits for every load of the one before).
-template <int OUTW, int K, int KR, int SB, int THREADS>
-__global__ __launch_bounds__(THREADS) void dfa_sparse_dyn_kernel(
+// The sparse form with its ids staged in LDS (round 4).  PMC of the
+// lock-step kernel above on the lines stream: the TA is ~75% busy, and two
+// things behind the steps cost more than their bytes (timing ablations,
+// snort, 1 GiB, dense u32; profiles/r04/dyn): the escape lookups -- an outt
+// load instruction for each of a block's 32 positions, almost every one
+// issued for a lane or two (6.51 -> 5.98 ms without them) -- and the id
+// stores, eight 16-B stores per lane per block, each instruction touching
+// 64 lines (6.51 -> 5.36 ms without them; with every lane's ids sent to one
+// L2-resident line 6.31: the lines' HBM traffic is not the cost).  Here:
+//  * each step writes its id, or for an escape its coded word, into the
+//    lane's staging row in LDS: one ds_write_b32 at an immediate offset,
+//    rows of 33 dwords so the 64 lanes of a step hit 64 banks; no register
+//    array holds the block's words;
+//  * escapes go in rounds over the lanes' escape masks: per round each
+//    lane with one left loads it (a round per escape of the lane with the
+//    most, ~2-4 per block, instead of 32 load instructions);
+//  * the block goes out transposed: store instruction t writes the 128-B
+//    line of chain 8t + lane / 8, chunk lane % 8 -- eight whole lines per
+//    instruction instead of 16-B pieces of 64 lines (NT: non-temporal).
+// Every loop a lane's exchange depends on is wave-uniform (lanes without a
+// segment or past their last block take part and store nothing).
+template <int OUTW, int KR, int THREADS, bool NT, int BU = 8>
+__global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
     const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
-    constexpr int SBW = OUTW ? SB : 4;
-    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 4];
-    __shared__ __attribute__((aligned(16))) uint32_t s_ids[THREADS * SBW];
+    constexpr int BLK = 32, SROW = 33;  // a lane's staging row: 32 ids + one pad dword
+    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 1];
+    __shared__ uint32_t s_ids[THREADS * SROW];
     if (KR) {
         const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
         const uint4* src = reinterpret_cast<const uint4*>(base);
@@ -1745,169 +1721,97 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_dyn_kernel(
         for (uint32_t k = threadIdx.x; k < nr * 64u; k += THREADS) dst[k] = src[k];
         __syncthreads();
     }
-    enum : uint32_t { REQ_NONE = 0, REQ_BLOCK = 1, REQ_WORD = 2, REQ_ESC = 3 };
+    const int lane = threadIdx.x & 63;
+    uint32_t* const my = s_ids + threadIdx.x * SROW;
+    const uint32_t* const wrows = s_ids + (threadIdx.x - lane) * SROW;  // the wave's rows
     const int64_t nseg = (n + seg_len - 1) / seg_len;
-    const int64_t sg = (int64_t)blockIdx.x * THREADS + threadIdx.x;  // at most one segment per lane (host)
-    bool live = sg < nseg;
-    const int64_t lo = live ? pos0 + sg * seg_len : 0;
-    const int64_t hi = live ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : 0;
-    int64_t p = lo - warm < stream_start ? stream_start : lo - warm;
-    if (!live) p = 0;
-    if (live && gram3) p = dfa_sync_lo(text, lo, p, gram3);
-    int64_t tw = p & ~(int64_t)15;  // the text window [tw, tw + 32): A, B
-    const tu32x4 zero4 = {0u, 0u, 0u, 0u};
-    tu32x4 A = live ? *reinterpret_cast<const tu32x4*>(text + tw) : zero4;
-    tu32x4 B = live && tw + 16 < hi ? *reinterpret_cast<const tu32x4*>(text + tw + 16) : zero4;
-    constexpr int TSYNC = 16 / (K + 1);  // wave steps between text refills
-    int tphase = 0;                      // wave-uniform
-    tu32x4 R[4] = {zero4, zero4, zero4, zero4};  // the aligned block of 8 record units holding state s
-    uint32_t s = 0, cb = 0xFFFFFFFFu, cnt = 0;
-    uint32_t req = REQ_NONE, nb = 0, escj = 0, V = 0;
-    const uint32_t* waddr = outt;  // a REQ_WORD / REQ_ESC load's address
-    bool fl = false;               // a staged block is complete: write it out at the end of the wave step
-    uint32_t fj = 0, fc = 0;       // its first slot (position - lo) and its positions
-    uint32_t* const stage = s_ids + threadIdx.x * SBW;
-    // staging slot of position offset j: 16-B chunks rotated by the lane, so
-    // lanes at the same slot hit different banks
-    auto slot = [&](uint32_t j) __attribute__((always_inline)) {
-        return ((((j >> 2) + threadIdx.x) & (SB / 4 - 1)) << 2) | (j & 3u);
-    };
-    auto staged = [&](uint32_t j) __attribute__((always_inline)) {
-        // the block of position offset j is complete once its last slot is
-        // staged (or the segment ends)
-        if ((j & (SB - 1)) == SB - 1 || lo + j + 1 == hi) {
-            fl = true;
-            fj = j & ~(uint32_t)(SB - 1);
-            fc = j - fj + 1;
-        }
-    };
-    // position p's transition word v: the state, the id, the count
-    auto complete = [&](uint32_t v) __attribute__((always_inline)) {
-        s = v & DFA_STATE_MASK;
-        const uint32_t code = v >> 20;
-        if (p >= lo) {
-            const uint32_t j = (uint32_t)(p - lo);
-            cnt += code != 0u;
-            if (OUTW) {
-                if (code == DFA_ESC) {
-                    req = REQ_ESC;
-                    escj = j;
-                    waddr = outt + s;
-                } else {
-                    stage[slot(j)] = code;
-                    staged(j);
+    const int64_t lanes = (int64_t)gridDim.x * THREADS;
+    uint32_t cnt = 0, cb = 0xFFFFFFFFu;
+    uint4 R[4] = {};
+    for (int64_t sg0 = (int64_t)blockIdx.x * THREADS + threadIdx.x; __ballot(sg0 < nseg); sg0 += lanes) {
+        const bool has = sg0 < nseg;
+        const int64_t lo = has ? pos0 + sg0 * seg_len : pos0 + n;
+        const int64_t hi = has ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : pos0 + n;
+        int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
+        if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
+        uint32_t s = 0;
+        for (int64_t i = wlo; i < lo; ++i) s = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, text[i], cb, R) & DFA_STATE_MASK;
+        const int64_t nblk = seg_len / BLK;
+        for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
+            bool act[2];
+            uint32_t WT[2][8];
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) {
+                act[tt] = lo + BLK * (b0 + tt) + BLK <= hi;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const tu32x4 w = act[tt] ? *reinterpret_cast<const tu32x4*>(text + lo + BLK * (b0 + tt) + 16 * q)
+                                             : tu32x4{0u, 0u, 0u, 0u};
+                    WT[tt][4 * q] = w.x;
+                    WT[tt][4 * q + 1] = w.y;
+                    WT[tt][4 * q + 2] = w.z;
+                    WT[tt][4 * q + 3] = w.w;
                 }
             }
-        }
-        ++p;
-    };
-    for (;;) {
-        // ---- the loads of the last wave step have landed: resolve them
-        if (req == REQ_BLOCK) cb = nb;  // the position is retried below
-        if (req == REQ_WORD) {
-            req = REQ_NONE;
-            complete(V);
-        } else if (req == REQ_ESC) {
-            req = REQ_NONE;
-            stage[slot(escj)] = V;
-            staged(escj);
-        } else {
-            req = REQ_NONE;
-        }
-        // ---- up to K positions per lane, no global load among them
+            if (!__ballot(act[0])) break;
+            unroll_for<0, 2>([&](auto tc) {
+                constexpr int tt = decltype(tc)::value;
+                if (tt == 1 && !__ballot(act[1])) return;
+                const int64_t b = b0 + tt;
+                uint32_t em = 0;  // this block's escapes
 #pragma unroll
-        for (int it = 0; it < K; ++it) {
-            if (live && req == REQ_NONE && !fl && p < hi) {
-                const uint32_t off = (uint32_t)(p - tw);  // < 32 (TSYNC)
-                const tu32x4 H = (off & 16u) ? B : A;
-                const uint32_t w01 = (off & 4u) ? H.y : H.x, w23 = (off & 4u) ? H.w : H.z;
-                const uint32_t c = (((off & 8u) ? w23 : w01) >> (8 * (off & 3u))) & 0xFFu;
-                if (s < F) {
-                    if (KR && s < (uint32_t)KR) {
-                        complete(s_rows[s * 256u + c]);
-                    } else {
-                        req = REQ_WORD;
-                        waddr = reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
-                    }
-                } else {
-                    const uint32_t rec = s - F, b = rec >> 3;
-                    if (b != cb) {
-                        req = REQ_BLOCK;  // this position again once the block is in
-                        nb = b;
-                    } else {
-                        // the 8-B unit form (pm_pack_sparse8): one unit {y, x0 | w << 9},
-                        // or two {y, x | 1 << 31}, {z, w} in the same block
-                        const uint32_t e = rec & 7u, key = c | 0x100u;
-                        const tu32x4 q = (e & 4u) ? ((e & 2u) ? R[3] : R[2]) : ((e & 2u) ? R[1] : R[0]);
-                        const uint32_t e2 = ((e >> 1) + 1u) & 3u;
-                        const tu32x4 q2 = (e2 & 2u) ? ((e2 & 1u) ? R[3] : R[2]) : ((e2 & 1u) ? R[1] : R[0]);
-                        const uint32_t y = (e & 1u) ? q.z : q.x, x = (e & 1u) ? q.w : q.y;
-                        uint32_t w = (x >> 9) & 0x3FFFFFu, hitv = y;
-                        bool hit = (x & 0x1FFu) == key;
-                        if (x >> 31) {
-                            const uint32_t z = (e & 1u) ? q2.x : q.z;
-                            if (!hit && ((x >> 16) & 0x1FFu) == key) {
-                                hit = true;
-                                hitv = z;
-                            }
-                            w = (e & 1u) ? q2.y : q.w;
-                        }
-                        if (hit) {
-                            complete(hitv);
-                        } else if (KR && w < (uint32_t)KR) {
-                            complete(s_rows[w * 256u + c]);
-                        } else {
-                            req = REQ_WORD;
-                            waddr = reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
-                        }
+                for (int j = 0; j < BLK; ++j) {
+                    const uint32_t v = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb, R);
+                    s = act[tt] ? v & DFA_STATE_MASK : s;
+                    cnt += act[tt] && v >= (1u << 20);  // a nonzero id (an escape is one)
+                    if (OUTW) {
+                        const bool esc = v >= (DFA_ESC << 20);
+                        my[j] = esc ? v : v >> 20;
+                        em |= esc ? 1u << j : 0u;
                     }
                 }
-            }
-        }
-        // ---- end of the wave step: write out complete staged blocks, issue
-        // every lane's load (waited for at the top of the next wave step)
-        if (OUTW && fl) {
-            const int64_t o = lo - pos0 + fj;
-            if (fc == (uint32_t)SB) {
-                tu32x4 v[SB / 4];
-#pragma unroll
-                for (int q = 0; q < SB / 4; ++q)
-                    v[q] = *reinterpret_cast<const tu32x4*>(stage + ((((uint32_t)q + threadIdx.x) & (SB / 4 - 1)) << 2));
+                if (!OUTW) return;
+                if (!act[tt]) em = 0;
+                while (__ballot(em != 0)) {  // one escape per lane per round
+                    if (em) {
+                        const uint32_t j = __builtin_ctz(em);
+                        em &= em - 1;
+                        my[j] = outt[my[j] & DFA_STATE_MASK];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
                 if (OUTW == 4) {
-                    tu32x4* dst = reinterpret_cast<tu32x4*>(reinterpret_cast<uint32_t*>(out) + o);
+                    const uint64_t am = __ballot(act[tt]);
+                    uint32_t* o = reinterpret_cast<uint32_t*>(out) + (sg0 - lane + (lane >> 3)) * seg_len + BLK * b +
+                                  4 * (lane & 7);
 #pragma unroll
-                    for (int q = 0; q < SB / 4; ++q) dst[q] = v[q];
-                } else {
-                    tu32x4* dst = reinterpret_cast<tu32x4*>(reinterpret_cast<uint16_t*>(out) + o);
+                    for (int t = 0; t < 8; ++t) {
+                        const int c = 8 * t + (lane >> 3);
+                        const uint32_t* src = wrows + c * SROW + 4 * (lane & 7);
+                        const tu32x4 v = {src[0], src[1], src[2], src[3]};
+                        if ((am >> c) & 1u) {
+                            if (NT) __builtin_nontemporal_store(v, reinterpret_cast<tu32x4*>(o));
+                            else *reinterpret_cast<tu32x4*>(o) = v;
+                        }
+                        o += 8 * seg_len;
+                    }
+                } else if (act[tt]) {  // u16 ids: the lane's own 64 B
+                    tu32x4* o = reinterpret_cast<tu32x4*>(reinterpret_cast<uint16_t*>(out) + (lo - pos0) + BLK * b);
 #pragma unroll
-                    for (int q = 0; q < SB / 8; ++q)
-                        dst[q] = tu32x4{v[2 * q].x | v[2 * q].y << 16, v[2 * q].z | v[2 * q].w << 16,
-                                        v[2 * q + 1].x | v[2 * q + 1].y << 16, v[2 * q + 1].z | v[2 * q + 1].w << 16};
+                    for (int q = 0; q < 4; ++q)
+                        o[q] = tu32x4{my[8 * q] | my[8 * q + 1] << 16, my[8 * q + 2] | my[8 * q + 3] << 16,
+                                      my[8 * q + 4] | my[8 * q + 5] << 16, my[8 * q + 6] | my[8 * q + 7] << 16};
                 }
-            } else {  // the segment's last, partial block
-                for (uint32_t j = 0; j < fc; ++j) put_id<OUTW>(out, o + j, stage[slot(fj + j)]);
-            }
-            fl = false;
+                __builtin_amdgcn_wave_barrier();
+            });
         }
-        if (req == REQ_BLOCK) {
-            const tu32x4* pb = reinterpret_cast<const tu32x4*>(base + F * 1024u + nb * 64u);
-            R[0] = pb[0];
-            R[1] = pb[1];
-            R[2] = pb[2];
-            R[3] = pb[3];
-        } else if (req != REQ_NONE) {
-            V = *waddr;
+        // the segment's last (< BLK) positions
+        for (int64_t i = lo + BLK * ((hi - lo) / BLK); i < hi; ++i) {
+            s = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, text[i], cb, R) & DFA_STATE_MASK;
+            const uint32_t v = outt[s];
+            if (OUTW) put_id<OUTW>(out, i - pos0, v);
+            cnt += v != 0u;
         }
-        if (++tphase == TSYNC) {  // wave-uniform: the text refill point
-            tphase = 0;
-            if (live && p >= tw + 16) {
-                A = B;
-                tw += 16;
-                if (tw + 16 < hi) B = *reinterpret_cast<const tu32x4*>(text + tw + 16);
-            }
-        }
-        live = p < hi || req != REQ_NONE;
-        if (!__ballot(live)) break;  // wave-uniform
     }
     if (count) {
         for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
@@ -2234,8 +2138,14 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // with registers capped for 6 waves per SIMD, 9 = (2) over the 8-B record
 // units of pm_pack_sparse8 (2 when the automaton has none), 10 = (9) with
 // the text of two blocks per load, 11 / 12 = (10) with the first 32 / 64
-// rows in LDS; -1 = the product choice: 12 for ids, 10 for count only, at
-// SDFA_LANES_PER_CU.  Side by side at 512 lanes per CU (snort, 1 GiB,
+// rows in LDS, 22-24 = timing ablations of (12)'s id output, 25-28 =
+// dfa_sparse_stage_kernel (ids staged in LDS, escapes in rounds, whole-line
+// stores; 27: 1024-lane workgroups with 16 LDS rows, 28: 27 with 4-unit
+// record blocks); -1 = the product choice: 28 for u32 ids, 12 for u16, 10
+// for count only, at SDFA_LANES_PER_CU.  Round 4, side by side (snort,
+// 1 GiB, dense u32, ms; profiles/r04/dyn): lines / shipped / ASCII
+//   12  6.50 / 4.60 / 5.19    27  6.17 / 4.40 / 5.00    28  6.19 / 4.10 / 4.11
+// (u16 ids: 27 and 28 are 3-8% slower than 12, which keeps them).  Side by side at 512 lanes per CU (snort, 1 GiB,
 // ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
 // rows are the round's first two-segment build, whose register arrays the
 // compiler had put in scratch):
@@ -2308,7 +2218,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw ? 12 : 10;
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw == 4 ? 28 : outw ? 12 : 10;
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
@@ -2332,30 +2242,33 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), b(DFA_THREADS);
-    if (lds_kernel && sdfa_lds >= 13 && sdfa_lds <= 18 && t.sbase8) {
-        // decoupled lanes (dfa_sparse_dyn_kernel): one segment per lane
-        // (seg above gives nseg <= lanes), DYN_THREADS lanes per workgroup
-        const int DT = sdfa_lds >= 16 ? 1024 : 256;
-        const dim3 g3d((unsigned)std::max<int64_t>(1, (nseg + DT - 1) / DT)), b3d(DT);
-#define DY(W, KK, R, S, T)                                                                                         \
-    hipLaunchKernelGGL((dfa_sparse_dyn_kernel<W, KK, R, S, T>), g3d, b3d, 0, s, text, stream_start, pos0, n, out, \
-                       count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-#define DYW(KK, R, S, T)                                   \
-    do {                                                   \
-        if (outw == 4) DY(4, KK, R, S, T);                 \
-        else if (outw == 2) DY(2, KK, R, S, T);            \
-        else DY(0, KK, R, S, T);                           \
-    } while (0)
-        switch (sdfa_lds) {
-            case 14: DYW(1, 0, 32, 256); break;
-            case 15: DYW(3, 0, 32, 256); break;
-            case 16: DYW(2, 64, 16, 1024); break;  // one workgroup per CU: 64 rows + 16-position staging
-            case 17: DYW(1, 64, 16, 1024); break;
-            case 18: DYW(3, 64, 16, 1024); break;
-            default: DYW(2, 0, 32, 256); break;  // 13
+    if (lds_kernel && sdfa_lds >= 25 && t.sbase8 && outw) {
+        // ids staged in LDS (dfa_sparse_stage_kernel): 25 / 26 = 512-lane
+        // workgroups, plain / non-temporal line stores; 27 = 1024-lane
+        // workgroups with 16 rows in LDS
+        const int ST = sdfa_lds >= 27 ? 1024 : 512;
+        int64_t wg = (nseg + ST - 1) / ST;
+        const int64_t cap = lanes / ST;
+        if (wg > cap) wg = cap;
+        if (wg < 1) wg = 1;
+        const dim3 gs((unsigned)wg), bs(ST);
+#define DST4(W)                                                                                                  \
+    hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, 16, 1024, false, 4>), gs, bs, 0, s, text, stream_start, pos0, n, \
+                       out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
+#define DST(W, K, T, N)                                                                                             \
+    hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, K, T, N>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, \
+                       t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
+        if (sdfa_lds == 26) {
+            if (outw == 4) DST(4, 0, 512, true); else DST(2, 0, 512, true);
+        } else if (sdfa_lds == 27) {
+            if (outw == 4) DST(4, 16, 1024, false); else DST(2, 16, 1024, false);
+        } else if (sdfa_lds == 28) {  // 27 with 4-unit (32-B) record blocks
+            if (outw == 4) DST4(4); else DST4(2);
+        } else {
+            if (outw == 4) DST(4, 0, 512, false); else DST(2, 0, 512, false);
         }
-#undef DY
-#undef DYW
+#undef DST
+#undef DST4
         return hipGetLastError();
     }
     if (lds_kernel) {
@@ -2379,9 +2292,6 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #define DL8K(W, K)                                                                                                    \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, K, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
                        count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-#define DL8X(K, X)                                                                                                 \
-    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, K, 1, 0, 8, 2, X>), g2, b2, 0, s, text, stream_start, pos0, n, \
-                       out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
 #define DLW(W, B, E)                                                                                                 \
     hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, 0, 1, E>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
                        t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr)
@@ -2426,17 +2336,26 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                     if (outw == 4) DL8K(4, 64); else if (outw == 2) DL8K(2, 64); else DL8K(0, 64);
                 }
                 break;
-            case 19:  // (10) with the ids through LDS as whole lines, non-temporal (u32 ids)
-            case 20:  // the same, plain stores
-            case 21:  // (12) with non-temporal whole-line ids
+            case 25:  // the staged-id kernels' count only: (10)
+            case 26:
+            case 27:
+            case 28:
+                if (outw == 4) DL8T(4); else if (outw == 2) DL8T(2); else DL8T(0);
+                break;
+            case 22:  // (12) with every block's ids to one line per lane (timing ablation, wrong ids)
+            case 23:  // (12) without escape lookups (timing ablation, wrong ids)
+            case 24:  // (12) with no id stores (timing ablation)
                 if (!t.sbase8 || outw != 4) {
                     if (outw == 4) DL8T(4); else if (outw == 2) DL8T(2); else DL8T(0);
-                } else if (sdfa_lds == 19) {
-                    DL8X(0, 1);
-                } else if (sdfa_lds == 20) {
-                    DL8X(0, 2);
+                } else if (sdfa_lds == 22) {
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, 64, 1, 0, 8, 2, 3>), g2, b2, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
+                } else if (sdfa_lds == 23) {
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, 64, 1, 0, 8, 2, 4>), g2, b2, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
                 } else {
-                    DL8X(64, 1);
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, 64, 1, 0, 8, 2, 5>), g2, b2, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
                 }
                 break;
             case 8:  // the same, registers capped for 6 waves per SIMD (three workgroups per CU)
@@ -2451,7 +2370,6 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #undef DL8
 #undef DL8T
 #undef DL8K
-#undef DL8X
         return hipGetLastError();
     }
     if (sparse) {
@@ -2529,7 +2447,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 21 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 28 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }

@@ -305,13 +305,16 @@ void ensure_slot(PmHip* o, PipeSlot& q, size_t positions) {
     q.cap = cap;
 }
 
-// Zero-copy small read_block calls (PM_HOST_ZC, a bit mask; timing A/B):
+// Zero-copy small read_block calls (PM_HOST_ZC, a bit mask, default 3):
 // 1 = the kernel writes its results straight into the pinned result buffer,
-// 2 = it reads the pinned staging buffer instead of a device copy.
+// 2 = it reads the pinned staging buffer instead of a device copy.  At the
+// reference's 100 KiB chunks (measure.c:77), per call, rt / ac gids: 65.6 /
+// 93.9 us with copies (0), 55.1 / 84.4 with 1, 48.2 / 76.5 with 3
+// (scripts/host_profile.py, profiles/r04/host_path).
 int host_zero_copy() {
     static const int z = [] {
         const char* e = std::getenv("PM_HOST_ZC");
-        return e ? (int)std::strtol(e, nullptr, 10) & 3 : 0;
+        return e ? (int)std::strtol(e, nullptr, 10) & 3 : 3;
     }();
     return z;
 }

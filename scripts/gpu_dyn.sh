@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); TAG=${1:-dyn}; OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 V=${2:-12,13,14,15,16,17,18}
 S=${3:-lines,ship,ascii}
-timeout -k 10 400 python scripts/sdfa_lds_ab.py --streams $S --modes dense,count --variants $V --rounds 3 \
+timeout -k 10 400 python scripts/sdfa_lds_ab.py --streams $S --modes ${MODES:-dense,count} --variants $V --rounds 3 --nocheck ${NOCHECK:-none} \
     > "$OUT/ab.json" 2> "$OUT/ab.err" || { tail -20 "$OUT/ab.err"; exit 1; }
 python3 -c "
 import json; d=json.load(open('$OUT/ab.json'))

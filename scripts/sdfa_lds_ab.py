@@ -22,6 +22,7 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--streams", default="lines,ship,ascii")
 ap.add_argument("--variants", default="0,1,2")
 ap.add_argument("--modes", default="dense")
+ap.add_argument("--nocheck", default="", help="timing ablations whose ids are not checked")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 WIDTH = {"dense": 4, "dense16": 2, "count": 0}
@@ -65,14 +66,14 @@ for st in args.streams.split(","):
                 if r:
                     times[v].append(e0.elapsed_time(e1))
                 counts[v] = int(cnt.item())
-                if r == 0 and w:
+                if r == 0 and w and str(v) not in args.nocheck.split(","):
                     h = int(outs[w][: n * w // 4].view(torch.int64)[:: 997].sum().item())
                     if ref is None:
                         ref = (h, outs[w][: n * w // 4].clone())
                     elif not torch.equal(ref[1], outs[w][: n * w // 4]):
                         raise SystemExit(f"{st} {mode}: variant {v} ids differ from variant {vs[0]}")
         del ref
-        assert len(set(counts.values())) == 1, counts
+        assert len({c for v, c in counts.items() if str(v) not in args.nocheck.split(",")}) <= 1, counts
         for v in vs:
             ms = statistics.median(times[v])
             res[f"{st}-{mode}-v{v}"] = {"ms": round(ms, 4), "stream_gbps": round(n / ms / 1e6, 1),

@@ -60,6 +60,7 @@ int main(int argc, char** argv) {
     for (auto& p : pats) { P.insert(P.end(), p.begin(), p.end()); O.push_back(P.size()); }
     const int KR = envi("KR", 64), WAVES = envi("WAVES", 64), SEG = envi("SEG", 4096), PF = envi("PF", 0);
     const int HOT = envi("HOT", 0);
+    const int BU = envi("BU", 8);  // record units per register block (8 = 64 B)
     printf("patterns %zu states %u rows F=%u units %zu maxlen %zu | KR %d HOT %d WAVES %d SEG %d PF %d\n",
            pats.size(), d.states, F, B8.size() / 2 - (size_t)F * 128, maxlen, KR, HOT, WAVES, SEG, PF);
     const int LANES = 64 * WAVES;
@@ -97,7 +98,7 @@ int main(int argc, char** argv) {
             if (inlds[s]) lds = 1; else { glob = 1; depth = 1; }
             return B8[(size_t)s * 256 + c];
         }
-        const uint32_t rec = s - F, b = rec >> 3;
+        const uint32_t rec = s - F, b = rec / BU;
         if (b != cb) { glob++; depth = 1; cb = b; blockload = true; }
         const uint32_t* U = B8.data() + (size_t)F * 256 + (size_t)rec * 2;
         const uint32_t key = c | 0x100u;
@@ -191,6 +192,9 @@ int main(int argc, char** argv) {
             printf("      decoupled K=%d: wave steps per segment %.0f (iterations %.0f) vs lock step %.0f\n", K,
                    wsteps / (double)WAVES, iters / (double)WAVES, wave_steps / (double)WAVES);
         }
+        printf("BU %d: TA lane-accesses per wave step %.1f (block %.1f + words %.1f)\n", BU,
+               64.0 * ((lane_glob - lane_blk) + lane_blk * (BU / 2.0)) / lane_steps * (lane_steps / (double)wave_steps) / 64.0 * 64.0 / 64.0 * 1.0,
+               64.0 * lane_blk * (BU / 2.0) / wave_steps, 64.0 * (lane_glob - lane_blk) / wave_steps);
         printf("%s lane steps %llu: LDS reads/step %.3f, global loads/step %.3f (block loads %.3f, %s%.3f), "
                "two dependent loads %.3f\n", pass ? "HOT " : "FIRST", (unsigned long long)lane_steps,
                lane_lds / (double)lane_steps, lane_glob / (double)lane_steps, lane_blk / (double)lane_steps,

@@ -232,7 +232,8 @@ def sdfa8_scan(img, text):
     (pm_pack_sparse8, pm_flatten.h): rows as in the 16-B form; state F + u
     is the record at unit u -- {y, x0 | w << 9} with one or no slot, or
     {y, x | 1 << 31}, {z, w} with two, never straddling an aligned block of
-    8 units.  Codes checked against sout8 at every step."""
+    4 units (32 B; so neither one of 8).  Codes checked against sout8 at
+    every step."""
     F = int(img.lib.pm_flat_dfa_sparse_rows(img.h))
     blk = img.array("sblock8")
     sout = img.array("sout8")
@@ -251,11 +252,11 @@ def sdfa8_scan(img, text):
             if xw & 0x1FF == key:
                 x = y
             elif xw >> 31 and (xw >> 16) & 0x1FF == key:
-                assert u % 8 != 7  # both units in one 64-B block
+                assert u % 4 != 3  # both units in one 32-B block
                 x = int(units[u + 1][0])
             else:
                 if xw >> 31:
-                    assert u % 8 != 7
+                    assert u % 4 != 3
                     w = int(units[u + 1][1])
                 else:
                     w = (xw >> 9) & 0x3FFFFF
