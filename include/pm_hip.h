@@ -233,6 +233,9 @@ void pm_hip_debug_spill_cap(int chunks);
 /* Timing sweeps only: at most b workgroups per reverse-trie launch (0 = one
  * per CU). */
 void pm_hip_debug_rt_blocks(int b);
+/* Timing sweeps / tests: reverse-trie launches of at most n positions use
+ * the one-thread-per-position kernel (0 = never; < 0 = the default). */
+void pm_hip_debug_rt_small(int64_t n);
 /* Timing only: the read_block host path's breakdown since the last call --
  * out5 = {staging s, enqueue s, wait s, result copy / map s, calls} -- then
  * reset and turn the accounting on (on != 0) or off. */

@@ -27,6 +27,7 @@ int64_t pm_rt_spill_items(int64_t n, int num_cu);
 // default), so small launches resolve full regions many times.
 void pm_rt_set_spill_cap(int chunks);
 void pm_rt_set_max_blocks(int b);  // timing sweeps: RT workgroups per launch (0 = one per CU)
+void pm_rt_set_small_max(int64_t n);  // launches of <= n positions use rt_small_kernel (0 = never, < 0 = default)
 
 struct DfaDev {
     const uint32_t* next;  // states * 256 (output-coded when coded, pm_flatten.h)

@@ -1098,6 +1098,32 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     }
 }
 
+// Small launches (the reference's 100 KiB read_block chunks, measure.c:77):
+// one thread per position, rt_one over the global tables -- no LDS tables to
+// stage, no chunk loop, no queue; a launch costs about one walk's chain of
+// dependent loads.  CONT positions (depth-2 node with children) count
+// towards spill_total, the auto kind's deep-input signal.
+constexpr int RT_SMALL_THREADS = 256;
+template <int OUTW>
+__global__ __launch_bounds__(RT_SMALL_THREADS) void rt_small_kernel(const uint8_t* __restrict__ text,
+                                                                    int64_t stream_start, int64_t pos0, int64_t n,
+                                                                    void* __restrict__ out,
+                                                                    unsigned long long* __restrict__ count, RtDev t) {
+    const int64_t k = (int64_t)blockIdx.x * RT_SMALL_THREADS + threadIdx.x;
+    uint32_t v = 0, deep = 0;
+    if (k < n) {
+        const int64_t i = pos0 + k;
+        v = rt_one(text, t.t12, t, i, stream_start);
+        if (i - stream_start >= 2) deep = (t.t12[(uint32_t)text[i] << 8 | text[i - 1]] & CONT16) != 0;
+        if (OUTW) put_id<OUTW>(out, k, v);
+    }
+    const uint64_t nz = __ballot(v != 0u), dp = __ballot(deep != 0u);
+    if ((threadIdx.x & 63) == 0) {
+        if (count && nz) atomicAdd(count, (unsigned long long)__popcll(nz));
+        if (t.spill_total && dp) atomicAdd(t.spill_total, (unsigned long long)__popcll(dp));
+    }
+}
+
 constexpr int DFA_THREADS = 256;
 
 template <int OUTW>
@@ -1968,6 +1994,9 @@ __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint6
 //   16 MiB:                              0.101 / 0.058 / 0.049 / 0.067
 //   64 MiB:                              0.366 / 0.193 / 0.116 / 0.104
 static int g_rt_max_blocks = 0;  // pm_rt_set_max_blocks (timing sweeps); 0 = the rule above
+// Launches of at most this many positions take rt_small_kernel
+// (pm_rt_set_small_max; 0 = never).
+static int64_t g_rt_small_max = (int64_t)256 << 10;
 static int64_t rt_blocks(int64_t n, int num_cu) {
     const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
     if (g_rt_max_blocks > 0) {
@@ -1982,6 +2011,7 @@ static int64_t rt_blocks(int64_t n, int num_cu) {
     return b < 1 ? 1 : b;
 }
 void pm_rt_set_max_blocks(int b) { g_rt_max_blocks = b > 0 ? b : 0; }
+void pm_rt_set_small_max(int64_t n) { g_rt_small_max = n >= 0 ? n : ((int64_t)256 << 10); }
 // Spill items per wave region: one per position of the wave's main-loop
 // chunks, capped at RT_SPILL_WAVE_CAP (the kernel resolves a full region
 // and goes on, rt_scan_kernel): 128 KiB per wave, 512 MiB for a 1 GiB launch
@@ -2024,6 +2054,13 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
+    }
+    if (variant == 0 && n <= g_rt_small_max) {  // small launch: one thread per position
+        const dim3 gs((unsigned)((n + RT_SMALL_THREADS - 1) / RT_SMALL_THREADS)), bs(RT_SMALL_THREADS);
+        if (outw == 4) hipLaunchKernelGGL(rt_small_kernel<4>, gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
+        else if (outw == 2) hipLaunchKernelGGL(rt_small_kernel<2>, gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
+        else hipLaunchKernelGGL(rt_small_kernel<0>, gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
+        return hipGetLastError();
     }
     const int64_t blocks = rt_blocks(n, num_cu);
     RtDev t = t0;

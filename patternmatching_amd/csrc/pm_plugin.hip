@@ -974,6 +974,7 @@ void pm_hip_debug_dfa_lds(int v) { pm_dfa_set_lds(v); }
 void pm_hip_debug_dfa_sync(int on) { pm_dfa_set_sync(on); }
 void pm_hip_debug_spill_cap(int chunks) { pm_rt_set_spill_cap(chunks); }
 void pm_hip_debug_rt_blocks(int b) { pm_rt_set_max_blocks(b); }
+void pm_hip_debug_rt_small(int64_t n) { pm_rt_set_small_max(n); }
 void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }
 void pm_hip_debug_dfa_min_seg(int min_seg) { pm_dfa_set_min_seg(min_seg); }
 

@@ -8,7 +8,7 @@ TRIES=${TRIES:-12}; WAIT=${WAIT:-150}
 for i in $(seq 1 $TRIES); do
   timeout $((LIM + 900)) /usr/local/graft/bin/gpurun --timeout "$LIM" -- "$CMD" > "$LOG" 2>&1
   rc=$?
-  if grep -q "status=transient" "$LOG" && grep -qE "no free box|backing off|stopped responding" "$LOG"; then
+  if grep -q "status=transient" "$LOG"; then
     w=$(grep -oE "retry in [0-9]+s" "$LOG" | grep -oE "[0-9]+" | tail -1)
     w=$(( ${w:-0} + 15 > WAIT ? ${w:-0} + 15 : WAIT ))
     echo "[when_free] attempt $i: no box ($(date +%T)); waiting $w s" >> "$LOG.tries"

@@ -181,8 +181,18 @@ def test_duplicate_add_pattern_last_id_wins(kind):
     m.free()
 
 
+@pytest.fixture(params=["chunked", "small"])
+def rt_small(request):
+    """RT launches of small sizes through the chunked kernel or the
+    one-thread-per-position kernel (pm_hip_debug_rt_small); both exact."""
+    lib = pm.load()
+    lib.pm_hip_debug_rt_small(0 if request.param == "chunked" else 1 << 40)
+    yield request.param
+    lib.pm_hip_debug_rt_small(-1)
+
+
 @pytest.mark.parametrize("kind", KINDS)
-def test_empty_and_ragged_inputs(kind):
+def test_empty_and_ragged_inputs(kind, rt_small):
     m = matcher("snort", kind)
     assert m.read_block_codes(b"").size == 0
     o = oracle_for("snort")
@@ -195,7 +205,7 @@ def test_empty_and_ragged_inputs(kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
-def test_kmp_kat(kind):
+def test_kmp_kat(kind, rt_small):
     """Core/src/kmprt.c:303-326: AAAAAAAAAAAAAAAAAB matches at 17 and 42."""
     d = pm.Dictionary([os.path.join(DATA, "kmp_kat.dict")])
     m = pm.HipMatcher(kind)
@@ -221,7 +231,7 @@ EDGE_DICTS = {
 
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("name", list(EDGE_DICTS))
-def test_edge_dictionaries_brute_force(name, kind):
+def test_edge_dictionaries_brute_force(name, kind, rt_small):
     pats = EDGE_DICTS[name]
     d = pm.Dictionary(patterns=pats)
     m = pm.HipMatcher(kind)
@@ -275,7 +285,7 @@ def test_device_generator_matches_host(kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
-def test_scan_device_shards_with_context(kind):
+def test_scan_device_shards_with_context(kind, rt_small):
     """Shard exactness: a shard scanned with max_len-1 bytes of context equals
     the same positions of one whole-stream scan."""
     torch = _torch()
