@@ -236,6 +236,20 @@ void pm_hip_debug_rt_blocks(int b);
 /* Timing sweeps / tests: reverse-trie launches of at most n positions use
  * the one-thread-per-position kernel (0 = never; < 0 = the default). */
 void pm_hip_debug_rt_small(int64_t n);
+/* Timing / tests: the one-thread-per-position kernel stages each
+ * workgroup's text window in LDS before its walks (1) or reads the text
+ * where it lies (0, the default). */
+void pm_hip_debug_rt_small_stage(int on);
+/* Timing only: read_block waits for its slots by polling the stream (1)
+ * or with hipStreamSynchronize (0); -1 = the default (PM_HOST_SPIN, 0). */
+void pm_hip_debug_host_spin(int on);
+/* Timing / tests: small read_block_gid calls (<= 256 Ki positions) bring
+ * u16 gids over the link and widen them on the host when every gid fits
+ * (gid16 = 1) or u32 gids (0, the default); small calls of either API time
+ * their launch with events for pm_hip_device_seconds (events = 1) or not
+ * (0, the default).  -1 restores a default (PM_HOST_GID16,
+ * PM_HOST_SMALL_EVENTS). */
+void pm_hip_debug_host_small(int gid16, int events);
 /* Timing only: the read_block host path's breakdown since the last call --
  * out5 = {staging s, enqueue s, wait s, result copy / map s, calls} -- then
  * reset and turn the accounting on (on != 0) or off. */

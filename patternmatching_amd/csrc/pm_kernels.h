@@ -17,6 +17,7 @@ struct RtDev {
     int64_t spill_stride;  // items per wave region, set per launch
     unsigned long long* spill_total;  // when set: += items spilled (the auto kernel choice)
     uint32_t t3h_bits;
+    uint32_t back;         // max pattern length - 1: the bytes a walk may read before its position
 };
 
 // Spill items (8 B each) an RT launch over n positions needs in
@@ -27,6 +28,7 @@ int64_t pm_rt_spill_items(int64_t n, int num_cu);
 // default), so small launches resolve full regions many times.
 void pm_rt_set_spill_cap(int chunks);
 void pm_rt_set_max_blocks(int b);  // timing sweeps: RT workgroups per launch (0 = one per CU)
+void pm_rt_set_small_stage(int on);  // timing: rt_small_kernel stages its text window in LDS (default 0)
 void pm_rt_set_small_max(int64_t n);  // launches of <= n positions use rt_small_kernel (0 = never, < 0 = default)
 
 struct DfaDev {

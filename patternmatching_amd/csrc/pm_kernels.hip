@@ -509,7 +509,9 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // as one byte per key, t8 = nz | cand << 1 (64 KiB, derived from t12
     // while staging), at LDS address 0: the 16-bit key (text[i] << 8 |
     // text[i-1]) is the byte address, one ds_read_u8, no base add or mask.
-    constexpr bool kT8 = V == 0 && OUTW == 0;
+    // (V = 13 / 14, count-only timing ablations: 13 drops the candidates
+    // after classification, 14 pushes them but skips the tail; wrong counts)
+    constexpr bool kT8 = (V == 0 || V == 13 || V == 14 || V == 15) && OUTW == 0;
     constexpr int kLdsWords = kT8 ? RT_T2_U16 / 4 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP
                                   : RT_FILTER_WORDS + RT_T2_U16 / 2 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP;
     __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsWords];
@@ -565,13 +567,15 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     //         V10 (no rounds, stage 2 in the tail's batched probe phase)
     //         0.733 / 0.832 / 8.63 (V9 on the same box 0.763 / 0.879 / 7.95)
     // So the product: u32 = V8, count = V10, u16 = issue-time stage 2.
-    constexpr bool kPushS2 = V == 8 || V == 9 || (V == 0 && OUTW == 4);
-    constexpr bool kRounds = !(V == 9 || V == 10 || ((V == 0 || V == 12) && OUTW == 0));
+    // (V = 15, count only: stage 2 at push time too, so only its passers
+    // go to the spill region)
+    constexpr bool kPushS2 = V == 8 || V == 9 || (V == 0 && OUTW == 4) || (V == 15 && OUTW == 0);
+    constexpr bool kRounds = !(V == 9 || V == 10 || ((V == 0 || V == 12 || V == 13 || V == 14 || V == 15) && OUTW == 0));
     // the stage-1 LDS filter; count-only without it (V = 0) queues every
     // zero-placeholder position under a depth-2 node with children (2.3%
     // of random-ASCII positions on snort) for the tail's batched stage 2
     // (V = 12 keeps it, timing)
-    constexpr bool kStage1 = !(V == 0 && OUTW == 0);
+    constexpr bool kStage1 = !((V == 0 || V == 13 || V == 14 || V == 15) && OUTW == 0);
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -843,7 +847,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         // every placeholder and spill store of this wave complete before
         // its walks patch or read them
         __builtin_amdgcn_s_waitcnt(0);
-        if (V == 6) {
+        if (V == 6 || V == 14) {
             cnt += sn;  // timing only: the chunk loop without the deep walks
         } else if (V == 3) {
             for (uint32_t k = lane; k < sn; k += 64) {
@@ -914,7 +918,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                 f |= (uint32_t)s_t8[key] << (2 * j);
             }
             cnt += (uint32_t)__popc(f & 0x55555555u);
-            cm = f & 0xAAAAAAAAu;
+            cm = V == 13 ? 0u : f & 0xAAAAAAAAu;
         } else {
 #pragma unroll
         for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
@@ -977,13 +981,13 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             // are queued (a rejected one keeps its depth-2 placeholder)
             uint32_t mm = cm, keep = 0;
             while (mm) {
-                const uint32_t j = __builtin_ctz(mm);
+                const uint32_t bit = __builtin_ctz(mm), j = bit >> CMS;
                 mm &= mm - 1;
                 const uint32_t sg = j >> 2, b = j & 3;
                 const u32x2 w01 = (sg & 1) ? x[1] : x[0], w23 = (sg & 1) ? x[3] : x[2];
                 const u32x2 w = (sg & 2) ? w23 : w01;
                 const uint32_t q32 = (uint32_t)((((uint64_t)w.y << 32) | w.x) >> (8 * (1 + b)));
-                keep |= (rt_stage2_hit(rt_stage2_load(s_f2, q32)) != 0u) << j;
+                keep |= (rt_stage2_hit(rt_stage2_load(s_f2, q32)) != 0u) << bit;
             }
             cm = keep;
         }
@@ -1103,18 +1107,54 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
 // stage, no chunk loop, no queue; a launch costs about one walk's chain of
 // dependent loads.  CONT positions (depth-2 node with children) count
 // towards spill_total, the auto kind's deep-input signal.
+// STAGE (an option, pm_rt_set_small_stage): the workgroup first copies its
+// text window -- its 256 positions and the RtDev::back bytes before them --
+// into LDS with dword loads issued together, and the walks read it there.
+// Meant for read_block's zero-copy calls, whose `text` is the pinned host
+// staging buffer, where each dependent byte read of a walk is a round trip
+// over the link; measured no faster there (the writes over the link, not
+// the reads, are what the call waits for).  Needs back <= RT_SMALL_BACK_MAX
+// and a 4-B aligned `text`.
 constexpr int RT_SMALL_THREADS = 256;
-template <int OUTW>
+constexpr int RT_SMALL_BACK_MAX = 512;  // the RT image's max_len <= 511 (pm_flatten.cpp)
+template <int OUTW, bool STAGE>
 __global__ __launch_bounds__(RT_SMALL_THREADS) void rt_small_kernel(const uint8_t* __restrict__ text,
                                                                     int64_t stream_start, int64_t pos0, int64_t n,
                                                                     void* __restrict__ out,
                                                                     unsigned long long* __restrict__ count, RtDev t) {
     const int64_t k = (int64_t)blockIdx.x * RT_SMALL_THREADS + threadIdx.x;
+    const uint8_t* tx = text;
+    if constexpr (STAGE) {
+        // window [lo, hi) of stream indices, staged from the 4-aligned word at or before lo
+        // (a walk that reaches a leaf at depth max_len reads the byte before
+        // it, unused: the window starts 4 bytes earlier, after one pad word,
+        // so every read stays inside s_win)
+        __shared__ uint32_t s_win[(RT_SMALL_THREADS + RT_SMALL_BACK_MAX + 32) / 4];
+        const int64_t i0 = pos0 + (int64_t)blockIdx.x * RT_SMALL_THREADS;
+        const int64_t lo = i0 - (int64_t)t.back - 4 > stream_start ? i0 - (int64_t)t.back - 4 : stream_start;
+        const int64_t hi = i0 + RT_SMALL_THREADS < pos0 + n ? i0 + RT_SMALL_THREADS : pos0 + n;
+        const int64_t w0 = lo >> 2;  // text is 4-B aligned: stream index 4w = word w
+        const uint32_t* tw = reinterpret_cast<const uint32_t*>(text);
+        for (int64_t w = w0 + threadIdx.x; 4 * w < hi; w += RT_SMALL_THREADS) {
+            uint32_t v;
+            if (4 * w >= lo && 4 * w + 4 <= hi) {
+                v = tw[w];
+            } else {  // a partial edge word: only bytes inside [lo, hi)
+                v = 0;
+                for (int b = 0; b < 4; ++b)
+                    if (4 * w + b >= lo && 4 * w + b < hi) v |= (uint32_t)text[4 * w + b] << (8 * b);
+            }
+            s_win[1 + w - w0] = v;
+        }
+        __syncthreads();
+        // a flat pointer whose [i] is s_win's byte of stream index i
+        tx = reinterpret_cast<const uint8_t*>(s_win + 1) - 4 * w0;
+    }
     uint32_t v = 0, deep = 0;
     if (k < n) {
         const int64_t i = pos0 + k;
-        v = rt_one(text, t.t12, t, i, stream_start);
-        if (i - stream_start >= 2) deep = (t.t12[(uint32_t)text[i] << 8 | text[i - 1]] & CONT16) != 0;
+        v = rt_one(tx, t.t12, t, i, stream_start);
+        if (i - stream_start >= 2) deep = (t.t12[(uint32_t)tx[i] << 8 | tx[i - 1]] & CONT16) != 0;
         if (OUTW) put_id<OUTW>(out, k, v);
     }
     const uint64_t nz = __ballot(v != 0u), dp = __ballot(deep != 0u);
@@ -1997,6 +2037,10 @@ static int g_rt_max_blocks = 0;  // pm_rt_set_max_blocks (timing sweeps); 0 = th
 // Launches of at most this many positions take rt_small_kernel
 // (pm_rt_set_small_max; 0 = never).
 static int64_t g_rt_small_max = (int64_t)256 << 10;
+// ... staging each workgroup's text window in LDS first (pm_rt_set_small_stage;
+// off: no faster at read_block's 100 KiB zero-copy calls, 40.6 against 39.3
+// us per call, profiles/r04/host_path/small_call_variants_ab.json)
+static bool g_rt_small_stage = false;
 static int64_t rt_blocks(int64_t n, int num_cu) {
     const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
     if (g_rt_max_blocks > 0) {
@@ -2012,6 +2056,7 @@ static int64_t rt_blocks(int64_t n, int num_cu) {
 }
 void pm_rt_set_max_blocks(int b) { g_rt_max_blocks = b > 0 ? b : 0; }
 void pm_rt_set_small_max(int64_t n) { g_rt_small_max = n >= 0 ? n : ((int64_t)256 << 10); }
+void pm_rt_set_small_stage(int on) { g_rt_small_stage = on != 0; }
 // Spill items per wave region: one per position of the wave's main-loop
 // chunks, capped at RT_SPILL_WAVE_CAP (the kernel resolves a full region
 // and goes on, rt_scan_kernel): 128 KiB per wave, 512 MiB for a 1 GiB launch
@@ -2057,9 +2102,20 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
     }
     if (variant == 0 && n <= g_rt_small_max) {  // small launch: one thread per position
         const dim3 gs((unsigned)((n + RT_SMALL_THREADS - 1) / RT_SMALL_THREADS)), bs(RT_SMALL_THREADS);
-        if (outw == 4) hipLaunchKernelGGL(rt_small_kernel<4>, gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
-        else if (outw == 2) hipLaunchKernelGGL(rt_small_kernel<2>, gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
-        else hipLaunchKernelGGL(rt_small_kernel<0>, gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
+        const bool stage = g_rt_small_stage && t0.back <= (uint32_t)RT_SMALL_BACK_MAX &&
+                           ((uintptr_t)text & 3) == 0;
+#define PM_RT_SMALL(W, ST) \
+    hipLaunchKernelGGL((rt_small_kernel<W, ST>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0)
+        if (stage) {
+            if (outw == 4) PM_RT_SMALL(4, true);
+            else if (outw == 2) PM_RT_SMALL(2, true);
+            else PM_RT_SMALL(0, true);
+        } else {
+            if (outw == 4) PM_RT_SMALL(4, false);
+            else if (outw == 2) PM_RT_SMALL(2, false);
+            else PM_RT_SMALL(0, false);
+        }
+#undef PM_RT_SMALL
         return hipGetLastError();
     }
     const int64_t blocks = rt_blocks(n, num_cu);
@@ -2109,6 +2165,9 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 9: RT_LAUNCH(9); break;
         case 10: RT_LAUNCH(10); break;
         case 12: RT_LAUNCH(12); break;
+        case 13: RT_LAUNCH_EF(13); break;
+        case 14: RT_LAUNCH_EF(14); break;
+        case 15: RT_LAUNCH_EF(15); break;
         default:
             // early prefetch for u16 ids and count only (0.864 -> 0.847 ms,
             // 0.565 -> 0.547); u32 ids would spill (1.166 -> 1.216)

@@ -119,6 +119,8 @@ struct PipeSlot {
     AutoPick pick;
     bool busy = false;
     bool staged = false;    // small block: results land in h_res, copied out by finish
+    bool timed = false;     // ev0 / ev1 bracket the launch (device seconds)
+    int w = 4;              // bytes per result position in h_res / d_res
     size_t off = 0, m = 0;  // block = positions [off, off + m) of the call
 };
 
@@ -319,6 +321,38 @@ int host_zero_copy() {
     return z;
 }
 
+// Waiting for a read_block slot by polling the stream (PM_HOST_SPIN=1,
+// pm_hip_debug_host_spin) instead of hipStreamSynchronize.
+int g_host_spin = -1;
+bool host_spin() {
+    if (g_host_spin < 0) {
+        const char* e = std::getenv("PM_HOST_SPIN");
+        g_host_spin = e ? (std::strtol(e, nullptr, 10) != 0) : 0;
+    }
+    return g_host_spin != 0;
+}
+
+// Small (staged) read_block_gid calls: u16 gids over the link, widened on
+// the host, when every gid < 65,536 (PM_HOST_GID16, default 0: the link
+// wait shrinks 3 us, the widening costs 5 us more than the copy), and
+// small calls' launches bracketed by timing events for
+// pm_hip_device_seconds (PM_HOST_SMALL_EVENTS, default 0: their two marker
+// packets cost ~2 us of a ~40 us call; profiles/r04/host_path/
+// small_call_variants_ab.json).  pm_hip_debug_host_small sets both.
+int g_gid16 = -1, g_small_events = -1;
+int env_int(const char* k, int d) {
+    const char* e = std::getenv(k);
+    return e ? (int)std::strtol(e, nullptr, 10) : d;
+}
+bool small_gid16() {
+    if (g_gid16 < 0) g_gid16 = env_int("PM_HOST_GID16", 0) != 0;
+    return g_gid16 != 0;
+}
+bool small_events() {
+    if (g_small_events < 0) g_small_events = env_int("PM_HOST_SMALL_EVENTS", 0) != 0;
+    return g_small_events != 0;
+}
+
 // Host threads for the copy/map work around the pipeline (PM_HOST_THREADS,
 // default min(8, hardware threads)).
 unsigned host_threads() {
@@ -505,7 +539,8 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
     PM_CHECK(hipSetDevice(o->device));
     const size_t keep = o->max_len ? o->max_len - 1 : 0;
     const size_t pipe = out_gid ? PIPE_GID_POSITIONS : PIPE_ID_POSITIONS;
-    const bool narrow = !out_gid && o->gids.index_of_gid.size() <= 65536;  // u16 gids over PCIe
+    const bool fits16 = o->gids.index_of_gid.size() <= 65536;
+    const bool narrow = !out_gid && fits16;  // u16 gids over PCIe
     o->last_out_width = narrow ? 2 : 4;
     double t_mark = g_hprof_on ? hp_now() : 0.0;
     auto lap = [&](int k) {
@@ -517,13 +552,25 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
     if (g_hprof_on) g_hprof[4] += 1;
     auto finish = [&](PipeSlot& q) {
         lap(1);
-        PM_CHECK(hipStreamSynchronize(q.stream));
+        if (host_spin()) {
+            hipError_t e;
+            while ((e = hipStreamQuery(q.stream)) == hipErrorNotReady) {}
+            PM_CHECK(e);
+        } else {
+            PM_CHECK(hipStreamSynchronize(q.stream));
+        }
         lap(2);
-        float ms = 0.f;
-        PM_CHECK(hipEventElapsedTime(&ms, q.ev0, q.ev1));
-        o->dev_seconds += ms * 1e-3;
+        if (q.timed) {
+            float ms = 0.f;
+            PM_CHECK(hipEventElapsedTime(&ms, q.ev0, q.ev1));
+            o->dev_seconds += ms * 1e-3;
+        }
         const pm_pattern_id_t* map = o->id_of_gid.data();
-        if (narrow) {
+        if (out_gid && q.staged && q.w == 2) {  // widen
+            const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
+            uint32_t* dst = out_gid + q.off;
+            for (size_t j = 0; j < q.m; ++j) dst[j] = g[j];
+        } else if (narrow) {
             const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
             pm_pattern_id_t* dst = out_ids + q.off;
             par_range(q.m, (size_t)1 << 18, [&](size_t lo, size_t hi) {
@@ -573,15 +620,18 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             PM_CHECK(hipMemcpyAsync(q.d_stage + ctx, buf + done, m, hipMemcpyHostToDevice, q.stream));
             PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
         }
-        PM_CHECK(hipEventRecord(q.ev0, q.stream));
+        q.w = narrow || (out_gid && q.staged && fits16 && small_gid16()) ? 2 : 4;
+        q.timed = !q.staged || small_events();
+        if (q.timed) PM_CHECK(hipEventRecord(q.ev0, q.stream));
         PM_CHECK(launch(o, zc_in ? q.h_stage : q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m,
-                        zc_out ? q.h_res : q.d_res, narrow ? 2 : 4, nullptr, q.stream, q.spill, q.spill_cap, q.pick));
+                        zc_out ? q.h_res : q.d_res, q.w, nullptr, q.stream, q.spill, q.spill_cap, q.pick));
         o->last_kernel = q.pick.last ? q.pick.last : o->kind;
         o->last_form = q.pick.last_form;
-        PM_CHECK(hipEventRecord(q.ev1, q.stream));
+        o->last_out_width = q.w;
+        if (q.timed) PM_CHECK(hipEventRecord(q.ev1, q.stream));
         if (zc_out)
             ;  // the results are in h_res once the stream is done
-        else if (narrow)
+        else if (q.w == 2)
             PM_CHECK(hipMemcpyAsync(q.h_res, q.d_res, m * sizeof(uint16_t), hipMemcpyDeviceToHost, q.stream));
         else
             PM_CHECK(hipMemcpyAsync(out_gid && !q.staged ? out_gid + done : q.h_res, q.d_res, m * sizeof(uint32_t),
@@ -656,6 +706,7 @@ void pm_hip_compile(void* obj) {
         o->rt.filt = (const uint32_t*)dalloc_copy(o, im.rt.filt.data(), im.rt.filt.size() * 4);
         o->rt.t3h = (const uint4*)dalloc_copy(o, im.rt.t3h.data(), im.rt.t3h.size() * 4);
         o->rt.t3h_bits = im.rt.t3h_bits;
+        o->rt.back = o->max_len ? o->max_len - 1 : 0;
         o->rt.rec = (const uint4*)dalloc_copy(o, im.rt.rec.data(), im.rt.rec.size() * 4);
         o->rt.wide = (const uint4*)dalloc_copy(o, im.rt.wide.data(), im.rt.wide.size() * 4);
         const std::vector<uint8_t> zero(RT_SCRATCH_BYTES, 0);
@@ -975,6 +1026,12 @@ void pm_hip_debug_dfa_sync(int on) { pm_dfa_set_sync(on); }
 void pm_hip_debug_spill_cap(int chunks) { pm_rt_set_spill_cap(chunks); }
 void pm_hip_debug_rt_blocks(int b) { pm_rt_set_max_blocks(b); }
 void pm_hip_debug_rt_small(int64_t n) { pm_rt_set_small_max(n); }
+void pm_hip_debug_rt_small_stage(int on) { pm_rt_set_small_stage(on); }
+void pm_hip_debug_host_spin(int on) { g_host_spin = on < 0 ? -1 : on != 0; }
+void pm_hip_debug_host_small(int gid16, int events) {
+    g_gid16 = gid16 < 0 ? -1 : gid16 != 0;
+    g_small_events = events < 0 ? -1 : events != 0;
+}
 void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }
 void pm_hip_debug_dfa_min_seg(int min_seg) { pm_dfa_set_min_seg(min_seg); }
 

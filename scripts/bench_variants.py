@@ -21,6 +21,7 @@ ap.add_argument("--variants", default="0,1,2")
 ap.add_argument("--modes", default="dense,dense16,count")
 ap.add_argument("--exact", default="", help="variants whose dense u32 ids must equal v0's (checked after timing)")
 ap.add_argument("--blocks", type=int, default=0, help="RT workgroups per launch (pm_hip_debug_rt_blocks; 0 = one per CU)")
+ap.add_argument("--counts", action="store_true", help="report each variant's match count of one launch (count mode)")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 WIDTH = {"dense": 4, "dense16": 2, "count": 0}
@@ -62,6 +63,12 @@ for (v, mode), t in times.items():
     ms = statistics.median(t)
     res[f"v{v}-{mode}"] = {"ms": round(ms, 4), "min": round(min(t), 4), "GBps_stream": round(n / ms / 1e6, 1),
                            "alg_GBps": round(n * (1 + WIDTH[mode]) / ms / 1e6, 1)}
+if args.counts:
+    for v in sorted({v for v, _ in variants}):
+        c1 = torch.zeros(1, dtype=torch.int64, device="cuda")
+        assert lib.pm_hip_debug_scan_variant(m.obj, v, text.data_ptr(), n, None, 0, c1.data_ptr(), s.cuda_stream) == 0
+        torch.cuda.synchronize()
+        res[f"v{v}-count-matches"] = int(c1.item())
 if args.exact:
     def ids(v):
         o = torch.zeros(n, dtype=torch.int32, device="cuda")

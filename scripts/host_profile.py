@@ -3,7 +3,12 @@
 size (measure.c:77 STREAM_BUFFER_SIZE = 100 KiB; measure.c:284 read_block per
 chunk): staging, enqueue (copies + launch), wait, result copy / id map, in
 microseconds per call (pm_hip_debug_host_profile), and the rate, for the rt
-and ac kinds, gids and pattern ids.  Prints one JSON object."""
+and ac kinds, gids and pattern ids.  PM_HOST_VARIANTS (e.g.
+"stage0,stage1,stage1spin") repeats it per setting of the small kernel's
+LDS text staging (pm_hip_debug_rt_small_stage) and the spin wait
+(pm_hip_debug_host_spin), u16 gids for small gid calls ("g16") and the
+per-call timing events ("ev": device_us is 0 without them,
+pm_hip_debug_host_small), side by side.  Prints one JSON object."""
 import ctypes
 import json
 import os
@@ -20,10 +25,16 @@ n = int(os.environ.get("PM_HOST_BYTES", 64 << 20))
 chunk = int(os.environ.get("PM_HOST_CHUNK", 100 << 10))
 text = pm.gen_stream(n, 1, 0)
 d = pm.Dictionary([os.path.join(DATA, "snort.dict")])
-res = {"stream_bytes": n, "chunk_bytes": chunk, "PM_HOST_ZC": os.environ.get("PM_HOST_ZC", "0")}
+res = {"stream_bytes": n, "chunk_bytes": chunk, "PM_HOST_ZC": os.environ.get("PM_HOST_ZC", "default 3")}
 lib = pm.load()
 prof = (ctypes.c_double * 5)()
-for kind in os.environ.get("PM_HOST_KINDS", "rt,ac").split(","):
+variants = os.environ.get("PM_HOST_VARIANTS", "")
+for var, kind in [(v, k) for v in (variants.split(",") if variants else [""])
+                  for k in os.environ.get("PM_HOST_KINDS", "rt,ac").split(",")]:
+    if var:
+        lib.pm_hip_debug_rt_small_stage(1 if "stage1" in var else 0)
+        lib.pm_hip_debug_host_spin(1 if "spin" in var else 0)
+        lib.pm_hip_debug_host_small(1 if "g16" in var else 0, 1 if "ev" in var else 0)
     m = pm.HipMatcher(kind)
     m.add_dictionary(d)
     m.compile()
@@ -46,7 +57,7 @@ for kind in os.environ.get("PM_HOST_KINDS", "rt,ac").split(","):
             dt = time.perf_counter() - t0
             lib.pm_hip_debug_host_profile(0, prof)
         calls = max(1.0, prof[4])
-        res[f"{kind}_{api}"] = {"GBps": round(n / dt / 1e9, 3), "us_per_call": round(dt / calls * 1e6, 2),
+        res[f"{kind}_{api}" + (f"_{var}" if var else "")] = {"GBps": round(n / dt / 1e9, 3), "us_per_call": round(dt / calls * 1e6, 2),
                                 "stage_us": round(prof[0] / calls * 1e6, 2),
                                 "enqueue_us": round(prof[1] / calls * 1e6, 2),
                                 "wait_us": round(prof[2] / calls * 1e6, 2),

@@ -181,14 +181,18 @@ def test_duplicate_add_pattern_last_id_wins(kind):
     m.free()
 
 
-@pytest.fixture(params=["chunked", "small"])
+@pytest.fixture(params=["chunked", "small", "small_lds"])
 def rt_small(request):
     """RT launches of small sizes through the chunked kernel or the
-    one-thread-per-position kernel (pm_hip_debug_rt_small); both exact."""
+    one-thread-per-position kernel (pm_hip_debug_rt_small), reading the text
+    where it lies (the default) or with its text window staged in LDS
+    (pm_hip_debug_rt_small_stage); all exact."""
     lib = pm.load()
     lib.pm_hip_debug_rt_small(0 if request.param == "chunked" else 1 << 40)
+    lib.pm_hip_debug_rt_small_stage(1 if request.param == "small_lds" else 0)
     yield request.param
     lib.pm_hip_debug_rt_small(-1)
+    lib.pm_hip_debug_rt_small_stage(0)
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -404,6 +408,40 @@ def test_u16_ids_refused_for_large_dictionaries():
     with pytest.raises(RuntimeError, match="65536"):
         m.scan_device(dt.data_ptr(), 0, 0, 4096, b.data_ptr(), None, torch.cuda.current_stream().cuda_stream,
                       out_width=2)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("key", ["snort", "70k"])
+def test_small_gid_calls_u16_and_u32(kind, key):
+    """Small read_block_gid calls (<= 256 Ki positions) bring u16 gids over
+    the link and widen them on the host when every gid fits, u32 otherwise
+    (a 70,000-pattern dictionary), with or without the per-call timing
+    events (pm_hip_debug_host_small): every form equals one large call."""
+    lib = pm.load()
+    if key == "snort":
+        m = matcher("snort", kind)
+        text = np.tile(SHIP, 1 + (600 << 10) // len(SHIP))[:600 << 10]
+    else:
+        pats = [b"%05dxq" % k for k in range(70000)]
+        m = pm.HipMatcher(kind)
+        m.add_dictionary(pm.Dictionary(patterns=pats))
+        m.compile()
+        rng = np.random.default_rng(3)
+        text = np.frombuffer(b"".join(pats[k] for k in rng.integers(0, 70000, size=90000)), np.uint8).copy()
+    m.reset()
+    whole = m.read_block_gids(text)  # > 256 Ki positions: u32 straight into the caller's array
+    if key == "70k":
+        assert whole.max() >= 65536
+    try:
+        for gid16, ev in ((1, 0), (0, 0), (1, 1)):
+            lib.pm_hip_debug_host_small(gid16, ev)
+            m.reset()
+            parts = [m.read_block_gids(text[o:o + (100 << 10)]) for o in range(0, len(text), 100 << 10)]
+            assert np.array_equal(np.concatenate(parts), whole), (gid16, ev)
+    finally:
+        lib.pm_hip_debug_host_small(-1, -1)
+    if key == "70k":
+        m.free()
 
 
 def _score_host(algo, real, parent, depth):
