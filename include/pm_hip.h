@@ -219,7 +219,9 @@ void pm_hip_debug_dfa_variant(int v);
  * 22 / 23 / 24 = (12) without HBM id lines / escape lookups / id stores
  * (timing ablations: wrong ids); 25 / 26 = ids staged in LDS and stored as
  * whole lines (plain / non-temporal), 27 = 25 with 1024-lane workgroups and
- * 16 rows in LDS, 28 = 27 with 4-unit (32-B) record blocks;
+ * 16 rows in LDS, 28 = 27 with 4-unit (32-B) record blocks, 29 / 30 / 31 =
+ * timing ablations of 28 (no escape lookups / no stores / neither staging
+ * nor stores; u32 ids only, wrong ids);
  * -1 = the product choice (28 for u32 ids, 12 for u16, 10 for count only). */
 void pm_hip_debug_dfa_lds(int v);
 /* Timing experiments only: 0 = every warm-up of the sparse form's product

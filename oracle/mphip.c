@@ -40,11 +40,20 @@ void mps_hip_register(void) {
 }
 #endif
 
+#ifdef PM_READ_BLOCK_HOOK
+/* the batch entry per slot that oracle/batch_measure.py's edit of the
+ * reference's loop calls (NULL: read_char per byte) */
+void (*mps_read_block[MPS_SIZE])(void*, const char*, size_t, pattern_id_t*);
+#endif
+
 /* kind: "rt", "ac" or "auto"; returns 0, or -1 for an unknown kind */
 int mps_hip_register_into(int slot, const char* kind) {
     if (!strcmp(kind, "rt")) reg(&mps_table[slot], "HIP Reverse-Trie", pm_hip_rt_create);
     else if (!strcmp(kind, "ac")) reg(&mps_table[slot], "HIP Aho-Corasick DFA", pm_hip_ac_create);
     else if (!strcmp(kind, "auto")) reg(&mps_table[slot], "HIP Auto (RT / AC per launch)", pm_hip_auto_create);
     else return -1;
+#ifdef PM_READ_BLOCK_HOOK
+    mps_read_block[slot] = (void (*)(void*, const char*, size_t, pattern_id_t*))pm_hip_read_block;
+#endif
     return 0;
 }

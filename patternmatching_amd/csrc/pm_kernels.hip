@@ -1807,7 +1807,9 @@ void dfa_sparse_lds_kernel(
 //    instruction instead of 16-B pieces of 64 lines (NT: non-temporal).
 // Every loop a lane's exchange depends on is wave-uniform (lanes without a
 // segment or past their last block take part and store nothing).
-template <int OUTW, int KR, int THREADS, bool NT, int BU = 8>
+// ABL (timing ablations, wrong ids): 1 = no escape lookups, 2 = no stores,
+// 3 = neither staging writes nor stores (the steps and the count alone).
+template <int OUTW, int KR, int THREADS, bool NT, int BU = 8, int ABL = 0>
 __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
@@ -1865,14 +1867,14 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
                     const uint32_t v = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb, R);
                     s = act[tt] ? v & DFA_STATE_MASK : s;
                     cnt += act[tt] && v >= (1u << 20);  // a nonzero id (an escape is one)
-                    if (OUTW) {
+                    if (OUTW && ABL != 3) {
                         const bool esc = v >= (DFA_ESC << 20);
                         my[j] = esc ? v : v >> 20;
                         em |= esc ? 1u << j : 0u;
                     }
                 }
-                if (!OUTW) return;
-                if (!act[tt]) em = 0;
+                if (!OUTW || ABL == 3) return;
+                if (!act[tt] || ABL == 1) em = 0;
                 while (__ballot(em != 0)) {  // one escape per lane per round
                     if (em) {
                         const uint32_t j = __builtin_ctz(em);
@@ -1881,7 +1883,9 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
-                if (OUTW == 4) {
+                if (ABL == 2) {
+                    cnt += my[lane & 31];  // the staged ids read back, not stored
+                } else if (OUTW == 4) {
                     const uint64_t am = __ballot(act[tt]);
                     uint32_t* o = reinterpret_cast<uint32_t*>(out) + (sg0 - lane + (lane >> 3)) * seg_len + BLK * b +
                                   4 * (lane & 7);
@@ -2378,7 +2382,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (lds_kernel && sdfa_lds >= 25 && t.sbase8 && outw) {
         // ids staged in LDS (dfa_sparse_stage_kernel): 25 / 26 = 512-lane
         // workgroups, plain / non-temporal line stores; 27 = 1024-lane
-        // workgroups with 16 rows in LDS
+        // workgroups with 16 rows in LDS; 29-31 = timing ablations of 28
         const int ST = sdfa_lds >= 27 ? 1024 : 512;
         int64_t wg = (nseg + ST - 1) / ST;
         const int64_t cap = lanes / ST;
@@ -2397,6 +2401,13 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             if (outw == 4) DST(4, 16, 1024, false); else DST(2, 16, 1024, false);
         } else if (sdfa_lds == 28) {  // 27 with 4-unit (32-B) record blocks
             if (outw == 4) DST4(4); else DST4(2);
+        } else if (sdfa_lds >= 29 && sdfa_lds <= 31) {  // timing ablations of 28 (u32 ids)
+#define DSTA(A)                                                                                                      \
+    hipLaunchKernelGGL((dfa_sparse_stage_kernel<4, 16, 1024, false, 4, A>), gs, bs, 0, s, text, stream_start, pos0, n, \
+                       out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
+            if (outw != 4) return hipErrorInvalidValue;
+            if (sdfa_lds == 29) DSTA(1); else if (sdfa_lds == 30) DSTA(2); else DSTA(3);
+#undef DSTA
         } else {
             if (outw == 4) DST(4, 0, 512, false); else DST(2, 0, 512, false);
         }
@@ -2580,7 +2591,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 28 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 31 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }

@@ -18,6 +18,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_SRC = "/root/reference/Core/src"
 REF_LOOP = os.path.join(REPO, "oracle", "_ref", "ref_loop")
+REF_LOOP_BATCHED = os.path.join(REPO, "oracle", "_ref", "ref_loop_batched")
 DATA = os.path.join(REPO, "tests", "golden", "data")
 needs_ref = pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference sources only in the build container")
 
@@ -50,16 +51,35 @@ def test_registration_stub_and_reference_loop_build():
     """mphip.c compiles against the reference's mps.h
     both ways: the unmodified enum, and with the maintainer's enum edit and
     read_block member."""
-    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "refloop"], capture_output=True, text=True)
+    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "refloop", "refloopb"], capture_output=True,
+                       text=True)
     assert r.returncode == 0, r.stderr
-    assert os.path.exists(REF_LOOP)
+    assert os.path.exists(REF_LOOP) and os.path.exists(REF_LOOP_BATCHED)
     r = subprocess.run(["gcc", "-fsyntax-only", "-w", f"-I{REF_SRC}", f"-I{os.path.join(REPO, 'include')}",
                         "-DMPS_HIP_RT=3", "-DMPS_HIP_AC=4", "-DMPS_HIP_AUTO=5",
                         os.path.join(REPO, "oracle", "mphip.c")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
 
 
-def _ref_loop(tmp_path, dict_names, stream_path, bg, lmac=None, timeout=600):
+@needs_ref
+def test_batch_edit_of_the_reference_loop(tmp_path):
+    """oracle/batch_measure.py makes exactly INTEGRATION.md §2's edit: the
+    per-byte loop of measure.c:292-294 becomes one read_block call when the
+    slot has one, the loop otherwise; everything else is unchanged."""
+    r = subprocess.run(["python3", os.path.join(REPO, "oracle", "batch_measure.py"), os.path.join(REF_SRC, "measure.c")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    orig = open(os.path.join(REF_SRC, "measure.c")).read()
+    edited = r.stdout
+    assert "mps_read_block[inst->algo](obj, stream_buffer, (size_t)len_read, algo_results);" in edited
+    assert edited.count("read_char_func(obj, stream_buffer[j])") == 1
+    import difflib
+    changed = [ln for ln in difflib.unified_diff(orig.splitlines(), edited.splitlines(), lineterm="", n=0)
+               if ln[:1] in "+-" and not ln.startswith(("+++", "---"))]
+    assert len(changed) <= 10, changed
+
+
+def _ref_loop(tmp_path, dict_names, stream_path, bg, lmac=None, timeout=600, exe=REF_LOOP):
     out = tmp_path / "results.csv"
     # write_stats_to_file opens O_WRONLY | O_CREAT with no mode (measure.c:348;
     # SURVEY App. A 3): create the file first so it stays readable
@@ -68,7 +88,7 @@ def _ref_loop(tmp_path, dict_names, stream_path, bg, lmac=None, timeout=600):
     env = dict(os.environ, PM_REF_BG=bg)
     if lmac:
         env["PM_REF_LMAC"] = lmac
-    args = [REF_LOOP]
+    args = [exe]
     for d in dict_names:
         args += ["-d", os.path.join(DATA, d)]
     args += ["-s", str(stream_path), "-o", str(out)]
@@ -116,3 +136,39 @@ def test_reference_loop_per_byte_rate(tmp_path):
             json.dump({"bytes": n, "stream": "seed-5 ascii", "dict": "snort.dict", "MBps_per_core": rates,
                        "what": "reference program loop (oracle/ref_loop.c), read_char per byte, clock() time"}, f)
     assert rates["HIP Reverse-Trie"] >= rates["Aho-Corasick"], rates
+
+
+@pytest.mark.gpu
+def test_reference_loop_with_the_batch_call_is_exact(tmp_path):
+    """The reference's program with INTEGRATION.md §2's batch call
+    (oracle/_ref/ref_loop_batched): every 100 KiB chunk of the loop
+    (measure.c:77, 284) goes to the GPU kernels through read_block, scored by
+    the reference's own measure_success_rate against its AC -- C1 (et.dict +
+    the shipped stream) and 16 MiB of snort ASCII, rt and auto slots: zero
+    false-positive, false-negative and partial rates."""
+    assert os.path.exists(REF_LOOP_BATCHED), "build it in the build container: make -C oracle refloopb"
+    import patternmatching_amd as pm
+    res = _ref_loop(tmp_path, ["et.dict"], os.path.join(DATA, "dictionaries_generated.stream"), "rt", "auto",
+                    exe=REF_LOOP_BATCHED)
+    assert set(res) == {"Aho-Corasick", "HIP Auto (RT / AC per launch)", "HIP Reverse-Trie"}, res.keys()
+    n = 16 << 20
+    stream = tmp_path / "ascii16M.stream"
+    pm.gen_stream(n, seed=5, mode=0).tofile(stream)
+    res2 = _ref_loop(tmp_path, ["snort.dict"], stream, "rt", "ac", timeout=900, exe=REF_LOOP_BATCHED)
+    secs = {}
+    for r in (res, res2):
+        for name, row in r.items():
+            assert float(row["False Positive Rate"]) == 0.0, (name, row)
+            assert float(row["False Negative Rate"]) == 0.0, (name, row)
+            assert float(row["Partial Success Rate"]) == 0.0, (name, row)
+    for name, row in res2.items():
+        secs[name] = float(row["Time (in secs)"])
+    ev = os.environ.get("PM_EVIDENCE_DIR")
+    if ev:
+        os.makedirs(ev, exist_ok=True)
+        with open(os.path.join(ev, "ref_loop_batched.json"), "w") as f:
+            json.dump({"bytes": n, "stream": "seed-5 ascii", "dict": "snort.dict", "clock_seconds": secs,
+                       "what": "reference program loop with INTEGRATION.md's batch call (oracle/_ref/ref_loop_batched): "
+                               "read_block per 100 KiB chunk for the HIP slots, read_char per byte for the reference "
+                               "AC; the CSV's Time column is clock(), process CPU time, which leaves out time the "
+                               "thread sleeps waiting for the GPU"}, f)
