@@ -511,12 +511,8 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // text[i-1]) is the byte address, one ds_read_u8, no base add or mask.
     // (V = 13 / 14, count-only timing ablations: 13 drops the candidates
     // after classification, 14 pushes them but skips the tail; wrong counts)
-    // (V = 16, count only: a 256-bit table of the bytes that are 1-byte
-    // patterns first -- such a position is nonzero whatever its key, and the
-    // 32-B table sits in 8 banks, so its reads never conflict -- and the
-    // class table read only by the other lanes)
-    constexpr bool kT8 = (V == 0 || V == 13 || V == 14 || V == 15 || V == 16 || V == 17) && OUTW == 0;
-    constexpr int kLdsWords = kT8 ? RT_T2_U16 / 4 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP + 8
+    constexpr bool kT8 = (V == 0 || V == 13 || V == 14 || V == 15) && OUTW == 0;
+    constexpr int kLdsWords = kT8 ? RT_T2_U16 / 4 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP
                                   : RT_FILTER_WORDS + RT_T2_U16 / 2 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP;
     __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsWords];
     uint32_t* const s_f = s_lds;
@@ -526,7 +522,6 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     uint32_t* const s_f2 = s_lds + (kT8 ? RT_T2_U16 / 4 : RT_FILTER_WORDS + RT_T2_U16 / 2);
     uint32_t(*const s_qkey)[RT_QCAP] = reinterpret_cast<uint32_t(*)[RT_QCAP]>(s_f2 + RT_F2_WORDS);
     uint32_t(*const s_qpos)[RT_QCAP] = s_qkey + RT_WAVES;
-    uint32_t* const s_one = s_f2 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP;  // kT8: 8 words
     {
         const uint4* fsrc = reinterpret_cast<const uint4*>(t.filt);
         if (kT8) {
@@ -541,11 +536,6 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
                     w |= (nz | cand << 1) << (8 * q);
                 }
                 s_lds[k] = w;
-            }
-            if ((V == 16 || V == 17) && threadIdx.x < 8) {
-                uint32_t w = 0;
-                for (int k = 0; k < 32; ++k) w |= (uint32_t)(t.t12[65536 + 32 * threadIdx.x + k] != 0) << k;
-                s_one[threadIdx.x] = w;
             }
         } else {
             const uint4* src = reinterpret_cast<const uint4*>(t.t12);
@@ -580,12 +570,12 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // (V = 15, count only: stage 2 at push time too, so only its passers
     // go to the spill region)
     constexpr bool kPushS2 = V == 8 || V == 9 || (V == 0 && OUTW == 4) || (V == 15 && OUTW == 0);
-    constexpr bool kRounds = !(V == 9 || V == 10 || ((V == 0 || V == 12 || V == 13 || V == 14 || V == 15 || V == 16 || V == 17) && OUTW == 0));
+    constexpr bool kRounds = !(V == 9 || V == 10 || ((V == 0 || V == 12 || V == 13 || V == 14 || V == 15) && OUTW == 0));
     // the stage-1 LDS filter; count-only without it (V = 0) queues every
     // zero-placeholder position under a depth-2 node with children (2.3%
     // of random-ASCII positions on snort) for the tail's batched stage 2
     // (V = 12 keeps it, timing)
-    constexpr bool kStage1 = !((V == 0 || V == 13 || V == 14 || V == 15 || V == 16 || V == 17) && OUTW == 0);
+    constexpr bool kStage1 = !((V == 0 || V == 13 || V == 14 || V == 15) && OUTW == 0);
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -923,34 +913,14 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             constexpr uint32_t kSel0 = 0x0C0C0000u;  // bytes 2, 3 = 0; byte 1 = text[i], byte 0 = text[i-1]
 #define RT_T8KEY(j) \
     __builtin_amdgcn_perm(x[(j) >> 2].y, x[(j) >> 2].x, kSel0 | (4u + ((j) & 3)) << 8 | (3u + ((j) & 3)))
-            if (V == 16 || V == 17) {
-                // bit j: position j's byte text[i] is a 1-byte pattern ({nz})
-                uint32_t ow[16], one = 0;
+            // (measured and removed, round 4: a conflict-free 256-bit table
+            // of the bytes that are 1-byte patterns read first, the class
+            // table only for the other lanes -- by exec mask or with those
+            // lanes on one broadcast address: exact, but 0.433 -> 0.647 /
+            // 0.668 ms on ASCII, the 16 extra LDS reads per chunk cost more
+            // than the conflicts they remove; profiles/r04/count_ablations)
 #pragma unroll
-                for (int j = 0; j < 16; ++j) ow[j] = s_one[(x[j >> 2].y >> (8 * (j & 3) + 5)) & 7u];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) one |= ((ow[j] >> ((x[j >> 2].y >> (8 * (j & 3))) & 31u)) & 1u) << j;
-                uint32_t cls[16];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    if (V == 16) {  // those lanes read byte 0 (one address: a broadcast, no conflict)
-                        const uint32_t o = (one >> j) & 1u, keep = o - 1u;  // keep: ~0 unless a 1-byte pattern
-                        cls[j] = ((uint32_t)s_t8[RT_T8KEY(j) & keep] & keep) | o;
-                    } else {  // those lanes skip the read (exec-masked)
-                        cls[j] = 1u;
-                        if (!((one >> j) & 1u)) {
-                            uint32_t k2 = RT_T8KEY(j);
-                            asm volatile("" : "+v"(k2));
-                            cls[j] = s_t8[k2];
-                        }
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 16; ++j) f |= cls[j] << (2 * j);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) f |= (uint32_t)s_t8[RT_T8KEY(j)] << (2 * j);
-            }
+            for (int j = 0; j < 16; ++j) f |= (uint32_t)s_t8[RT_T8KEY(j)] << (2 * j);
 #undef RT_T8KEY
             cnt += (uint32_t)__popc(f & 0x55555555u);
             cm = V == 13 ? 0u : f & 0xAAAAAAAAu;
@@ -2207,8 +2177,6 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         case 13: RT_LAUNCH_EF(13); break;
         case 14: RT_LAUNCH_EF(14); break;
         case 15: RT_LAUNCH_EF(15); break;
-        case 16: RT_LAUNCH_EF(16); break;
-        case 17: RT_LAUNCH_EF(17); break;
         default:
             // early prefetch for u16 ids and count only (0.864 -> 0.847 ms,
             // 0.565 -> 0.547); u32 ids would spill (1.166 -> 1.216)
