@@ -170,14 +170,23 @@ PmGidMap pm_assign_gids(const std::vector<std::string>& pats) {
     g.gid_of_index.assign(P, 0);
     g.index_of_gid.assign(1, 0);
     g.index_of_gid.reserve(P + 1);
-    for (int pass = 0; pass < 2; ++pass)
-        for (size_t k = 0; k < P; ++k) {
-            bool short_pat = pats[k].size() <= 2;
-            if ((pass == 0) == short_pat) {
-                g.gid_of_index[k] = (uint32_t)g.index_of_gid.size();
-                g.index_of_gid.push_back((uint32_t)k);
-            }
-        }
+    // Patterns of <= 2 bytes first (the reverse trie's depth-2 answers are
+    // 15-bit gids below RT_CONT16), then the rest by length, shortest first,
+    // in add order within a length: a position's output is the longest
+    // pattern ending there, so short patterns are the frequent outputs, and
+    // the coded DFA words carry gids < DFA_ESC inline (a larger one is an
+    // escape, looked up per position).  On the snort lines stream 13.7% of
+    // the nonzero outputs escaped in add order, 9.8% in this order.
+    std::vector<uint32_t> order(P);
+    for (size_t k = 0; k < P; ++k) order[k] = (uint32_t)k;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        const size_t la = pats[a].size() <= 2 ? 0 : pats[a].size(), lb = pats[b].size() <= 2 ? 0 : pats[b].size();
+        return la < lb;
+    });
+    for (uint32_t k : order) {
+        g.gid_of_index[k] = (uint32_t)g.index_of_gid.size();
+        g.index_of_gid.push_back(k);
+    }
     return g;
 }
 
@@ -508,7 +517,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 10;                    // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 11;                    // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);
