@@ -248,8 +248,9 @@ void pm_hip_debug_host_spin(int on);
 /* Timing / tests: small read_block_gid calls (<= 256 Ki positions) bring
  * u16 gids over the link and widen them on the host when every gid fits
  * (gid16 = 1) or u32 gids (0, the default); small calls of either API time
- * their launch with events for pm_hip_device_seconds (events = 1) or not
- * (0, the default).  -1 restores a default (PM_HOST_GID16,
+ * their launch with events for pm_hip_device_seconds (events = 1, the
+ * default) or not (0: ~2 us faster per call, but pm_hip_device_seconds
+ * then leaves small calls out).  -1 restores a default (PM_HOST_GID16,
  * PM_HOST_SMALL_EVENTS). */
 void pm_hip_debug_host_small(int gid16, int events);
 /* Timing only: the read_block host path's breakdown since the last call --

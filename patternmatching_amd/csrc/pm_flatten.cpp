@@ -171,17 +171,81 @@ PmGidMap pm_assign_gids(const std::vector<std::string>& pats) {
     g.index_of_gid.assign(1, 0);
     g.index_of_gid.reserve(P + 1);
     // Patterns of <= 2 bytes first (the reverse trie's depth-2 answers are
-    // 15-bit gids below RT_CONT16), then the rest by length, shortest first,
-    // in add order within a length: a position's output is the longest
-    // pattern ending there, so short patterns are the frequent outputs, and
-    // the coded DFA words carry gids < DFA_ESC inline (a larger one is an
-    // escape, looked up per position).  On the snort lines stream 13.7% of
-    // the nonzero outputs escaped in add order, 9.8% in this order.
+    // 15-bit gids below RT_CONT16), then the rest by how often each is a
+    // position's output, most often first: the coded DFA words carry gids <
+    // DFA_ESC inline, and a larger one is an escape, looked up per position
+    // (the sparse kernels' largest single cost on pattern-dense input).
+    // The weight of pattern p: over the trie states whose output (the
+    // longest pattern that is a suffix of the state's string, mpac.c:272's
+    // rule) is p, the number of patterns below the state -- how often
+    // pattern-dense text, which walks the patterns' own paths, visits them.
+    // Share of the nonzero outputs that escape, 16 MiB of snort (lines
+    // stream / shipped stream): add order 13.7% / 11.3%, by length 9.8% /
+    // 6.1%, by this weight 5.1% / 1.4% (the best any order reaches on the
+    // lines stream is 5.0%); random ASCII ~0 in every order.
+    std::unordered_map<uint64_t, uint32_t> edge;
+    size_t total = 0;
+    for (const auto& p : pats) total += p.size();
+    edge.reserve(total + 1);
+    std::vector<uint32_t> parent(1, 0);
+    std::vector<uint8_t> inbyte(1, 0);
+    std::vector<uint16_t> depth(1, 0);
+    std::vector<int64_t> term(1, -1);
+    for (size_t k = 0; k < P; ++k) {
+        uint32_t v = 0;
+        for (unsigned char c : pats[k]) {
+            const uint64_t key = (uint64_t)v << 8 | c;
+            auto it = edge.find(key);
+            if (it == edge.end()) {
+                const uint32_t w = (uint32_t)parent.size();
+                edge.emplace(key, w);
+                parent.push_back(v);
+                inbyte.push_back(c);
+                depth.push_back((uint16_t)std::min<size_t>(depth[v] + 1, 65535));
+                term.push_back(-1);
+                v = w;
+            } else {
+                v = it->second;
+            }
+        }
+        if (!pats[k].empty()) term[v] = (int64_t)k;  // a repeated pattern: the later one is the output
+    }
+    const uint32_t N = (uint32_t)parent.size();
+    std::vector<uint64_t> sub(N, 0);  // patterns at or below each state (a child's id exceeds its parent's)
+    for (uint32_t v = 0; v < N; ++v) sub[v] = term[v] >= 0;
+    for (uint32_t v = N; v-- > 1;) sub[parent[v]] += sub[v];
+    std::vector<uint32_t> bfs(N);
+    for (uint32_t v = 0; v < N; ++v) bfs[v] = v;
+    std::stable_sort(bfs.begin(), bfs.end(), [&](uint32_t a, uint32_t b) { return depth[a] < depth[b]; });
+    std::vector<uint32_t> fail(N, 0);
+    std::vector<int64_t> outp(N, -1);
+    std::vector<uint64_t> weight(P, 0);
+    for (uint32_t v : bfs) {
+        if (v == 0) continue;
+        const uint32_t p = parent[v];
+        if (p != 0) {
+            uint32_t f = fail[p];
+            for (;;) {
+                auto it = edge.find((uint64_t)f << 8 | inbyte[v]);
+                if (it != edge.end()) {
+                    fail[v] = it->second;
+                    break;
+                }
+                if (f == 0) break;
+                f = fail[f];
+            }
+        }
+        outp[v] = term[v] >= 0 ? term[v] : outp[fail[v]];
+        if (outp[v] >= 0) weight[(size_t)outp[v]] += sub[v];
+    }
     std::vector<uint32_t> order(P);
     for (size_t k = 0; k < P; ++k) order[k] = (uint32_t)k;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-        const size_t la = pats[a].size() <= 2 ? 0 : pats[a].size(), lb = pats[b].size() <= 2 ? 0 : pats[b].size();
-        return la < lb;
+        const bool sa = pats[a].size() <= 2, sb = pats[b].size() <= 2;
+        if (sa != sb) return sa;
+        if (sa) return false;  // add order among the short ones
+        if (weight[a] != weight[b]) return weight[a] > weight[b];
+        return pats[a].size() < pats[b].size();
     });
     for (uint32_t k : order) {
         g.gid_of_index[k] = (uint32_t)g.index_of_gid.size();
@@ -517,7 +581,7 @@ DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
 namespace {
 
 constexpr uint64_t IMG_MAGIC = 0x31474D494D500000ull;  // "\0\0PMIMG1"
-constexpr uint32_t IMG_VERSION = 11;                    // bump when a table layout changes
+constexpr uint32_t IMG_VERSION = 12;                    // bump when a table layout changes
 
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = static_cast<const uint8_t*>(p);

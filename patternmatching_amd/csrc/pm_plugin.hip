@@ -336,8 +336,9 @@ bool host_spin() {
 // the host, when every gid < 65,536 (PM_HOST_GID16, default 0: the link
 // wait shrinks 3 us, the widening costs 5 us more than the copy), and
 // small calls' launches bracketed by timing events for
-// pm_hip_device_seconds (PM_HOST_SMALL_EVENTS, default 0: their two marker
-// packets cost ~2 us of a ~40 us call; profiles/r04/host_path/
+// pm_hip_device_seconds (PM_HOST_SMALL_EVENTS, default 1; without them a
+// call saves ~2 us of ~40 but pm_hip_device_seconds -- the CSV's GPU
+// columns -- leaves small calls out; profiles/r04/host_path/
 // small_call_variants_ab.json).  pm_hip_debug_host_small sets both.
 int g_gid16 = -1, g_small_events = -1;
 int env_int(const char* k, int d) {
@@ -349,7 +350,7 @@ bool small_gid16() {
     return g_gid16 != 0;
 }
 bool small_events() {
-    if (g_small_events < 0) g_small_events = env_int("PM_HOST_SMALL_EVENTS", 0) != 0;
+    if (g_small_events < 0) g_small_events = env_int("PM_HOST_SMALL_EVENTS", 1) != 0;
     return g_small_events != 0;
 }
 
