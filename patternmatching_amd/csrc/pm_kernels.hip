@@ -1779,7 +1779,7 @@ void dfa_sparse_lds_kernel(
 // segment or past their last block take part and store nothing).
 // ABL (timing ablations, wrong ids): 1 = no escape lookups, 2 = no stores,
 // 3 = neither staging writes nor stores (the steps and the count alone).
-template <int OUTW, int KR, int THREADS, bool NT, int BU = 8, int ABL = 0, int ESCK = 1>
+template <int OUTW, int KR, int THREADS, bool NT, int BU = 8, int ABL = 0>
 __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
@@ -1845,29 +1845,14 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
                 }
                 if (!OUTW || ABL == 3) return;
                 if (!act[tt] || ABL == 1) em = 0;
-                if (ESCK == 1) {
-                    while (__ballot(em != 0)) {  // one escape per lane per round
-                        if (em) {
-                            const uint32_t j = __builtin_ctz(em);
-                            em &= em - 1;
-                            my[j] = outt[my[j] & DFA_STATE_MASK];
-                        }
-                    }
-                } else {
-                    while (__ballot(em != 0)) {  // up to ESCK escapes per lane per round, loads in flight together
-                        uint32_t jj[ESCK], w[ESCK];
-#pragma unroll
-                        for (int q = 0; q < ESCK; ++q) {
-                            jj[q] = em ? __builtin_ctz(em) : 32u;
-                            em &= em - 1;
-                        }
-#pragma unroll
-                        for (int q = 0; q < ESCK; ++q) w[q] = jj[q] < 32u ? my[jj[q]] : 0u;
-#pragma unroll
-                        for (int q = 0; q < ESCK; ++q) w[q] = jj[q] < 32u ? outt[w[q] & DFA_STATE_MASK] : 0u;
-#pragma unroll
-                        for (int q = 0; q < ESCK; ++q)
-                            if (jj[q] < 32u) my[jj[q]] = w[q];
+                // (measured and removed: 4 / 8 escapes per lane per round,
+                // their loads in flight together -- lines 5.75 -> 5.73 /
+                // 5.72 ms, shipped 3.86 -> 3.86 / 3.89; profiles/r04/gid_order)
+                while (__ballot(em != 0)) {  // one escape per lane per round
+                    if (em) {
+                        const uint32_t j = __builtin_ctz(em);
+                        em &= em - 1;
+                        my[j] = outt[my[j] & DFA_STATE_MASK];
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -2268,6 +2253,8 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // for count only, at SDFA_LANES_PER_CU.  Round 4, side by side (snort,
 // 1 GiB, dense u32, ms; profiles/r04/dyn): lines / shipped / ASCII
 //   12  6.50 / 4.60 / 5.19    27  6.17 / 4.40 / 5.00    28  6.19 / 4.10 / 4.11
+// and 28 with gids numbered by output frequency (pm_assign_gids: 5.1% of
+// the lines stream's outputs escape instead of 13.7%): 5.75 / 3.86 / 4.10.
 // (u16 ids: 27 and 28 are 3-8% slower than 12, which keeps them).  Side by side at 512 lanes per CU (snort, 1 GiB,
 // ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
 // rows are the round's first two-segment build, whose register arrays the
@@ -2378,9 +2365,6 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
 #define DST4(W)                                                                                                  \
     hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, 16, 1024, false, 4>), gs, bs, 0, s, text, stream_start, pos0, n, \
                        out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-#define DSTE(W, E)                                                                                                  \
-    hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, 16, 1024, false, 4, 0, E>), gs, bs, 0, s, text, stream_start, pos0,   \
-                       n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
 #define DST(W, K, T, N)                                                                                             \
     hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, K, T, N>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, \
                        t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
@@ -2390,12 +2374,6 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             if (outw == 4) DST(4, 16, 1024, false); else DST(2, 16, 1024, false);
         } else if (sdfa_lds == 28) {  // 27 with 4-unit (32-B) record blocks
             if (outw == 4) DST4(4); else DST4(2);
-        } else if (sdfa_lds == 32 || sdfa_lds == 33) {  // 28 with 4 / 8 escapes per lane per round
-            if (outw == 4) {
-                if (sdfa_lds == 32) DSTE(4, 4); else DSTE(4, 8);
-            } else {
-                if (sdfa_lds == 32) DSTE(2, 4); else DSTE(2, 8);
-            }
         } else if (sdfa_lds >= 29 && sdfa_lds <= 31) {  // timing ablations of 28 (u32 ids)
 #define DSTA(A)                                                                                                      \
     hipLaunchKernelGGL((dfa_sparse_stage_kernel<4, 16, 1024, false, 4, A>), gs, bs, 0, s, text, stream_start, pos0, n, \
@@ -2407,7 +2385,6 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             if (outw == 4) DST(4, 0, 512, false); else DST(2, 0, 512, false);
         }
 #undef DST
-#undef DSTE
 #undef DST4
         return hipGetLastError();
     }
@@ -2587,7 +2564,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 33 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 31 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }
