@@ -41,6 +41,7 @@ struct DfaDev {
     uint32_t sF;           // states with full rows
     const uint8_t* sbase8;  // the same with 8-B record units (pm_pack_sparse8), or null
     const uint32_t* sout8;  // its ids' outputs
+    const uint16_t* sout8h; // the same as u16 when every gid < 65536 (else null)
     // 2^24-bit set of the 3-byte strings occurring in some pattern (bit
     // t[q] | t[q+1] << 8 | t[q+2] << 16), or null.  A 3-gram outside it is
     // synchronizing: the state after it is the root's over those 3 bytes

@@ -1779,11 +1779,14 @@ void dfa_sparse_lds_kernel(
 // segment or past their last block take part and store nothing).
 // ABL (timing ablations, wrong ids): 1 = no escape lookups, 2 = no stores,
 // 3 = neither staging writes nor stores (the steps and the count alone).
-template <int OUTW, int KR, int THREADS, bool NT, int BU = 8, int ABL = 0>
+// O16: the escapes read the u16 copy of the output table (DfaDev::sout8h;
+// half its L2 footprint: lines 5.69 -> 5.61 ms).
+template <int OUTW, int KR, int THREADS, bool NT, int BU = 8, int ABL = 0, bool O16 = false>
 __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
-    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
+    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3,
+    const uint16_t* __restrict__ outt16 = nullptr) {
     constexpr int BLK = 32, SROW = 33;  // a lane's staging row: 32 ids + one pad dword
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 1];
     __shared__ uint32_t s_ids[THREADS * SROW];
@@ -1845,14 +1848,14 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
                 }
                 if (!OUTW || ABL == 3) return;
                 if (!act[tt] || ABL == 1) em = 0;
-                // (measured and removed: 4 / 8 escapes per lane per round,
-                // their loads in flight together -- lines 5.75 -> 5.73 /
-                // 5.72 ms, shipped 3.86 -> 3.86 / 3.89; profiles/r04/gid_order)
+                // (measured and removed: up to 4 / 8 escapes per lane per
+                // round, their loads issued together -- no faster, lines 5.75
+                // -> 5.74 / 5.75 ms; profiles/r04/gid_order)
                 while (__ballot(em != 0)) {  // one escape per lane per round
                     if (em) {
                         const uint32_t j = __builtin_ctz(em);
                         em &= em - 1;
-                        my[j] = outt[my[j] & DFA_STATE_MASK];
+                        my[j] = O16 ? (uint32_t)outt16[my[j] & DFA_STATE_MASK] : outt[my[j] & DFA_STATE_MASK];
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -2249,12 +2252,15 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // rows in LDS, 22-24 = timing ablations of (12)'s id output, 25-28 =
 // dfa_sparse_stage_kernel (ids staged in LDS, escapes in rounds, whole-line
 // stores; 27: 1024-lane workgroups with 16 LDS rows, 28: 27 with 4-unit
-// record blocks); -1 = the product choice: 28 for u32 ids, 12 for u16, 10
+// record blocks; 34: 28 with the u16 escape table); -1 = the product
+// choice: 34 (28 without a u16 table) for u32 ids, 12 for u16, 10
 // for count only, at SDFA_LANES_PER_CU.  Round 4, side by side (snort,
 // 1 GiB, dense u32, ms; profiles/r04/dyn): lines / shipped / ASCII
 //   12  6.50 / 4.60 / 5.19    27  6.17 / 4.40 / 5.00    28  6.19 / 4.10 / 4.11
 // and 28 with gids numbered by output frequency (pm_assign_gids: 5.1% of
-// the lines stream's outputs escape instead of 13.7%): 5.75 / 3.86 / 4.10.
+// the lines stream's outputs escape instead of 13.7%): 5.75 / 3.86 / 4.10;
+// 34 = 28 with the u16 escape table (the product when every gid fits):
+// 5.61 / 3.80 / 4.10 against 5.69 / 3.80 / 4.07 side by side.
 // (u16 ids: 27 and 28 are 3-8% slower than 12, which keeps them).  Side by side at 512 lanes per CU (snort, 1 GiB,
 // ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
 // rows are the round's first two-segment build, whose register arrays the
@@ -2328,7 +2334,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw == 4 ? 28 : outw ? 12 : 10;
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw == 4 ? (t.sout8h ? 34 : 28) : outw ? 12 : 10;
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
@@ -2374,6 +2380,13 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             if (outw == 4) DST(4, 16, 1024, false); else DST(2, 16, 1024, false);
         } else if (sdfa_lds == 28) {  // 27 with 4-unit (32-B) record blocks
             if (outw == 4) DST4(4); else DST4(2);
+        } else if (sdfa_lds == 34) {  // 28 with the u16 escape table
+            if (!t.sout8h) return hipErrorInvalidValue;
+#define DSTH(W)                                                                                                     \
+    hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, 16, 1024, false, 4, 0, true>), gs, bs, 0, s, text, stream_start, \
+                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3, t.sout8h)
+            if (outw == 4) DSTH(4); else DSTH(2);
+#undef DSTH
         } else if (sdfa_lds >= 29 && sdfa_lds <= 31) {  // timing ablations of 28 (u32 ids)
 #define DSTA(A)                                                                                                      \
     hipLaunchKernelGGL((dfa_sparse_stage_kernel<4, 16, 1024, false, 4, A>), gs, bs, 0, s, text, stream_start, pos0, n, \
@@ -2564,7 +2577,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 31 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 34 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }

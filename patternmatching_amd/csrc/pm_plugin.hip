@@ -747,6 +747,10 @@ void pm_hip_compile(void* obj) {
                 b8.resize(b8.size() + 16, 0u);  // the last aligned 64-B block
                 o->dfa.sbase8 = (const uint8_t*)dalloc_copy(o, b8.data(), b8.size() * 4);
                 o->dfa.sout8 = (const uint32_t*)dalloc_copy(o, o8.data(), o8.size() * 4);
+                if (o->gids.index_of_gid.size() <= 65536) {  // half the escape table's footprint in L2
+                    std::vector<uint16_t> h(o8.begin(), o8.end());
+                    o->dfa.sout8h = (const uint16_t*)dalloc_copy(o, h.data(), h.size() * 2);
+                }
             }
         }
     }
