@@ -1900,6 +1900,115 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
     }
 }
 
+// dfa_sparse_stage_kernel with u16 staging rows (u32 ids out; every gid <
+// 65536): a lane's row is 17 dwords (32 u16 ids + pad; 17 is odd, so the
+// 64 lanes of a step still hit 64 banks), half of the 32-bit rows, and the
+// LDS that frees holds KR fallback rows instead of 16 (the model, scripts/
+// sdfa_wave_model.cpp, lines stream: 1.91 dependent loads per wave step with
+// 16 rows, 1.77 with 80).  An escape's slot holds the low 16 bits of its
+// state, the high 4 bits sit in four registers (hi4, 8 positions each).
+template <int KR, int BU>
+__global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
+    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* __restrict__ out,
+    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
+    const uint32_t* __restrict__ outt, const uint16_t* __restrict__ outt16, int64_t warm, int64_t seg_len,
+    const uint32_t* __restrict__ gram3) {
+    constexpr int THREADS = 1024, BLK = 32, SROW = 17;
+    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
+    __shared__ uint32_t s_ids[THREADS * SROW];
+    {
+        const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_rows);
+        for (uint32_t k = threadIdx.x; k < nr * 64u; k += THREADS) dst[k] = src[k];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    uint16_t* const my = reinterpret_cast<uint16_t*>(s_ids + threadIdx.x * SROW);
+    const uint32_t* const wrows = s_ids + (threadIdx.x - lane) * SROW;  // the wave's rows
+    const int64_t nseg = (n + seg_len - 1) / seg_len;
+    const int64_t lanes = (int64_t)gridDim.x * THREADS;
+    uint32_t cnt = 0, cb = 0xFFFFFFFFu;
+    uint4 R[4] = {};
+    for (int64_t sg0 = (int64_t)blockIdx.x * THREADS + threadIdx.x; __ballot(sg0 < nseg); sg0 += lanes) {
+        const bool has = sg0 < nseg;
+        const int64_t lo = has ? pos0 + sg0 * seg_len : pos0 + n;
+        const int64_t hi = has ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : pos0 + n;
+        int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
+        if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
+        uint32_t s = 0;
+        for (int64_t i = wlo; i < lo; ++i) s = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, text[i], cb, R) & DFA_STATE_MASK;
+        const int64_t nblk = seg_len / BLK;
+        for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
+            bool act[2];
+            uint32_t WT[2][8];
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) {
+                act[tt] = lo + BLK * (b0 + tt) + BLK <= hi;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const tu32x4 w = act[tt] ? *reinterpret_cast<const tu32x4*>(text + lo + BLK * (b0 + tt) + 16 * q)
+                                             : tu32x4{0u, 0u, 0u, 0u};
+                    WT[tt][4 * q] = w.x;
+                    WT[tt][4 * q + 1] = w.y;
+                    WT[tt][4 * q + 2] = w.z;
+                    WT[tt][4 * q + 3] = w.w;
+                }
+            }
+            if (!__ballot(act[0])) break;
+            unroll_for<0, 2>([&](auto tc) {
+                constexpr int tt = decltype(tc)::value;
+                if (tt == 1 && !__ballot(act[1])) return;
+                const int64_t b = b0 + tt;
+                uint32_t em = 0, hi4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int j = 0; j < BLK; ++j) {
+                    const uint32_t v = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb, R);
+                    s = act[tt] ? v & DFA_STATE_MASK : s;
+                    cnt += act[tt] && v >= (1u << 20);  // a nonzero id (an escape is one)
+                    const bool esc = v >= (DFA_ESC << 20);
+                    my[j] = (uint16_t)(esc ? v : v >> 20);
+                    hi4[j >> 3] |= esc ? ((v >> 16) & 0xFu) << (4 * (j & 7)) : 0u;
+                    em |= esc ? 1u << j : 0u;
+                }
+                if (!act[tt]) em = 0;
+                while (__ballot(em != 0)) {  // one escape per lane per round
+                    if (em) {
+                        const uint32_t j = __builtin_ctz(em);
+                        em &= em - 1;
+                        const uint32_t h = j < 16 ? (j < 8 ? hi4[0] : hi4[1]) : (j < 24 ? hi4[2] : hi4[3]);
+                        my[j] = outt16[my[j] | ((h >> (4 * (j & 7))) & 0xFu) << 16];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                const uint64_t am = __ballot(act[tt]);
+                uint32_t* o = out + (sg0 - lane + (lane >> 3)) * seg_len + BLK * b + 4 * (lane & 7);
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int c = 8 * t + (lane >> 3);
+                    const uint32_t* src = wrows + c * SROW + 2 * (lane & 7);
+                    const uint32_t w0 = src[0], w1 = src[1];
+                    const tu32x4 v = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
+                    if ((am >> c) & 1u) *reinterpret_cast<tu32x4*>(o) = v;
+                    o += 8 * seg_len;
+                }
+                __builtin_amdgcn_wave_barrier();
+            });
+        }
+        // the segment's last (< BLK) positions
+        for (int64_t i = lo + BLK * ((hi - lo) / BLK); i < hi; ++i) {
+            s = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, text[i], cb, R) & DFA_STATE_MASK;
+            const uint32_t v = outt[s];
+            out[i - pos0] = v;
+            cnt += v != 0u;
+        }
+    }
+    if (count) {
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
+    }
+}
+
 // Accuracy of one id stream against a reference one (Core/src/measure.c:
 // 174-190 with is_pattern_suffix, PatternsTree.c:485-494), one position per
 // lane-element: equal -> success; algo on real's parent chain -> partial;
@@ -2252,15 +2361,19 @@ static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64
 // rows in LDS, 22-24 = timing ablations of (12)'s id output, 25-28 =
 // dfa_sparse_stage_kernel (ids staged in LDS, escapes in rounds, whole-line
 // stores; 27: 1024-lane workgroups with 16 LDS rows, 28: 27 with 4-unit
-// record blocks; 34: 28 with the u16 escape table); -1 = the product
-// choice: 34 (28 without a u16 table) for u32 ids, 12 for u16, 10
+// record blocks; 34: 28 with the u16 escape table; 35 / 36: u16 staging
+// rows with 88 / 48 LDS rows); -1 = the product choice: 35 (28 without a
+// u16 table) for u32 ids, 12 for u16, 10
 // for count only, at SDFA_LANES_PER_CU.  Round 4, side by side (snort,
 // 1 GiB, dense u32, ms; profiles/r04/dyn): lines / shipped / ASCII
 //   12  6.50 / 4.60 / 5.19    27  6.17 / 4.40 / 5.00    28  6.19 / 4.10 / 4.11
 // and 28 with gids numbered by output frequency (pm_assign_gids: 5.1% of
 // the lines stream's outputs escape instead of 13.7%): 5.75 / 3.86 / 4.10;
-// 34 = 28 with the u16 escape table (the product when every gid fits):
-// 5.61 / 3.80 / 4.10 against 5.69 / 3.80 / 4.07 side by side.
+// 34 = 28 with the u16 escape table: 5.61 / 3.80 / 4.10 against 5.69 /
+// 3.80 / 4.07 side by side; 35 / 36 = dfa_sparse_stage16_kernel (u16
+// staging rows, 88 / 48 LDS rows; the product for u32 ids when every gid
+// fits is 35): 5.58 / 3.75 / 3.77 and 5.64 / 3.87 / 4.00 against 34's
+// 5.63 / 3.85 / 4.08 (profiles/r04/gid_order/stage16_ab.json).
 // (u16 ids: 27 and 28 are 3-8% slower than 12, which keeps them).  Side by side at 512 lanes per CU (snort, 1 GiB,
 // ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
 // rows are the round's first two-segment build, whose register arrays the
@@ -2334,7 +2447,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw == 4 ? (t.sout8h ? 34 : 28) : outw ? 12 : 10;
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw == 4 ? (t.sout8h ? 35 : 28) : outw ? 12 : 10;
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
@@ -2380,7 +2493,14 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             if (outw == 4) DST(4, 16, 1024, false); else DST(2, 16, 1024, false);
         } else if (sdfa_lds == 28) {  // 27 with 4-unit (32-B) record blocks
             if (outw == 4) DST4(4); else DST4(2);
-        } else if (sdfa_lds == 34) {  // 28 with the u16 escape table
+        } else if ((sdfa_lds == 35 || sdfa_lds == 36) && outw == 4) {  // u16 staging rows, 88 / 48 LDS rows
+            if (!t.sout8h) return hipErrorInvalidValue;
+#define DS16(K)                                                                                                     \
+    hipLaunchKernelGGL((dfa_sparse_stage16_kernel<K, 4>), gs, bs, 0, s, text, stream_start, pos0, n,                   \
+                       reinterpret_cast<uint32_t*>(out), count, t.sbase8, t.sF, t.sout8, t.sout8h, t.warm, seg, g3)
+            if (sdfa_lds == 35) DS16(88); else DS16(48);
+#undef DS16
+        } else if (sdfa_lds >= 34) {  // 28 with the u16 escape table (and 35 / 36 for u16 ids)
             if (!t.sout8h) return hipErrorInvalidValue;
 #define DSTH(W)                                                                                                     \
     hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, 16, 1024, false, 4, 0, true>), gs, bs, 0, s, text, stream_start, \
@@ -2577,7 +2697,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 34 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 36 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }

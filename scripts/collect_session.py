@@ -43,7 +43,7 @@ if os.path.exists(p):
     drd, dwr = d["FETCH_SIZE"] * 1024, d["WRITE_SIZE"] * 1024
     tr["snort-lines-1073741824-dense-auto"] = {
         "source": f"{rel}/pmc_deep_summary.json (rocprofv3 --pmc, one counter per pass, median over dispatches of "
-                  "the sparse AC-DFA kernel the auto kind holds on the lines stream, dfa_sparse_stage_kernel; "
+                  "the sparse AC-DFA kernel the auto kind holds on the lines stream, dfa_sparse_stage16_kernel<88, 4>; "
                   "1 dispatch per 1 GiB step)",
         "read_bytes_raw": drd, "write_bytes": dwr, "traffic_bytes": drd + dwr,
         "algorithmic_bytes": (1 << 30) * 5,

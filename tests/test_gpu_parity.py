@@ -805,9 +805,9 @@ def test_sparse_dfa_kernel_variants_agree(stream):
     lib.pm_hip_debug_dfa_sparse(1)
     try:
         for size, start in ((n, 0), (777, 4096), (100 << 10, 12345 & ~15), (5 << 20, 3 << 20)):
-            for form, lanes, sync in [(f, ln, y) for f in list(range(13)) + [25, 26, 27, 28, 34]
+            for form, lanes, sync in [(f, ln, y) for f in list(range(13)) + [25, 26, 27, 28, 34, 35, 36]
                                       for ln in ((512, 1024, 1536) if f in (2, 8, 9, 10, 12, 25, 27, 28) else (0,))
-                                      for y in ((0, 1) if f in (10, 11, 12, 25, 27, 28, 34) else (0,))]:
+                                      for y in ((0, 1) if f in (10, 11, 12, 25, 27, 28, 34, 35) else (0,))]:
                     lib.pm_hip_debug_dfa_lds(form)
                     lib.pm_hip_debug_dfa_shape(lanes)
                     lib.pm_hip_debug_dfa_sync(sync)
@@ -857,7 +857,7 @@ def test_dfa_warmups_stop_at_stream_start(stream):
             buf[stream_start:] = dt[: n + 64 - stream_start]
             ref = torch.empty(size, dtype=torch.int32, device="cuda")
             rt.scan_device(buf.data_ptr(), stream_start, pos0, size, ref.data_ptr(), None, s)
-            forms = [(0, -1, y) for y in (0, 1)] + [(1, f, y) for f in (0, 2, 10, 12, 25, 27, 28, 34) for y in (0, 1)]
+            forms = [(0, -1, y) for y in (0, 1)] + [(1, f, y) for f in (0, 2, 10, 12, 25, 27, 28, 34, 35) for y in (0, 1)]
             for sparse, lds, sync in forms:
                 lib.pm_hip_debug_dfa_sparse(sparse)
                 lib.pm_hip_debug_dfa_lds(lds)
