@@ -2493,12 +2493,14 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             if (outw == 4) DST(4, 16, 1024, false); else DST(2, 16, 1024, false);
         } else if (sdfa_lds == 28) {  // 27 with 4-unit (32-B) record blocks
             if (outw == 4) DST4(4); else DST4(2);
-        } else if ((sdfa_lds == 35 || sdfa_lds == 36) && outw == 4) {  // u16 staging rows, 88 / 48 LDS rows
+        } else if (sdfa_lds >= 35 && sdfa_lds <= 36 && outw == 4) {  // u16 staging rows, 88 / 48 LDS rows
+            // (measured and removed: 64-B record blocks here, 5.60 -> 5.84
+            // lines, 3.76 -> 4.12 shipped, 3.80 -> 4.79 ASCII; profiles/r04/gid_order/stage16_blocks64_ab.json)
             if (!t.sout8h) return hipErrorInvalidValue;
-#define DS16(K)                                                                                                     \
-    hipLaunchKernelGGL((dfa_sparse_stage16_kernel<K, 4>), gs, bs, 0, s, text, stream_start, pos0, n,                   \
+#define DS16(K, B)                                                                                                  \
+    hipLaunchKernelGGL((dfa_sparse_stage16_kernel<K, B>), gs, bs, 0, s, text, stream_start, pos0, n,                   \
                        reinterpret_cast<uint32_t*>(out), count, t.sbase8, t.sF, t.sout8, t.sout8h, t.warm, seg, g3)
-            if (sdfa_lds == 35) DS16(88); else DS16(48);
+            if (sdfa_lds == 35) DS16(88, 4); else DS16(48, 4);
 #undef DS16
         } else if (sdfa_lds >= 34) {  // 28 with the u16 escape table (and 35 / 36 for u16 ids)
             if (!t.sout8h) return hipErrorInvalidValue;
