@@ -256,6 +256,11 @@ void pm_hip_debug_host_spin(int on);
  * then leaves small calls out).  -1 restores a default (PM_HOST_GID16,
  * PM_HOST_SMALL_EVENTS). */
 void pm_hip_debug_host_small(int gid16, int events);
+/* Timing / tests: small read_block calls copy / map their results on a
+ * persistent pool of host workers (> 0; the pool, once made, keeps the
+ * size it was made with) or on the calling thread alone (0); -1 = the
+ * default (PM_HOST_POOL, 3). */
+void pm_hip_debug_host_pool(int workers);
 /* Timing only: the read_block host path's breakdown since the last call --
  * out5 = {staging s, enqueue s, wait s, result copy / map s, calls} -- then
  * reset and turn the accounting on (on != 0) or off. */

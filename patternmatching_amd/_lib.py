@@ -125,6 +125,7 @@ SIGNATURES = {
     "pm_hip_debug_rt_small_stage": (None, [ctypes.c_int]),
     "pm_hip_debug_host_spin": (None, [ctypes.c_int]),
     "pm_hip_debug_host_small": (None, [ctypes.c_int, ctypes.c_int]),
+    "pm_hip_debug_host_pool": (None, [ctypes.c_int]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
     "pm_flat_build_cached": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int,

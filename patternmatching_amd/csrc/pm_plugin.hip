@@ -18,7 +18,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -366,6 +370,114 @@ unsigned host_threads() {
     return t;
 }
 
+// A small persistent pool for the result copy / id map of small read_block
+// calls (the reference's 100 KiB chunks, measure.c:77), whose ~10-27 us of
+// single-threaded host work is a quarter to a half of the call: a thread
+// per piece per call would cost more than the piece.  Workers spin on a
+// ticket for up to PM_HOST_POOL_SPIN_US (default 200) microseconds after
+// their last piece -- so back-to-back calls find them awake -- then sleep
+// on a condition variable.  A job is one generation of the ticket (gen <<
+// 40 | pieces << 20 | next piece); a worker runs a piece only after
+// claiming it by CAS in that generation, so the job's function stays valid
+// while it runs (the caller waits for every piece before returning).
+// PM_HOST_POOL = the workers (default 3; 0 = off: the caller does it all).
+class HostPool {
+public:
+    explicit HostPool(unsigned workers) {
+        const char* e = std::getenv("PM_HOST_POOL_SPIN_US");
+        spin_us_ = e ? std::max(0L, std::strtol(e, nullptr, 10)) : 200L;
+        for (unsigned i = 0; i < workers; ++i) std::thread([this] { loop(); }).detach();
+        workers_ = workers;
+    }
+    unsigned workers() const { return workers_; }
+    // f(k) for k in [0, pieces) on the workers and the caller; returns when all are done
+    void run(unsigned pieces, const std::function<void(unsigned)>& f) {
+        std::lock_guard<std::mutex> g(submit_);
+        fn_.store(&f, std::memory_order_relaxed);
+        pending_.store(pieces, std::memory_order_relaxed);
+        const uint64_t gen = (ticket_.load(std::memory_order_relaxed) >> 40) + 1;
+        ticket_.store(gen << 40 | (uint64_t)pieces << 20, std::memory_order_seq_cst);
+        if (sleepers_.load(std::memory_order_seq_cst)) {
+            std::lock_guard<std::mutex> l(m_);
+            cv_.notify_all();
+        }
+        work(gen);
+        while (pending_.load(std::memory_order_acquire)) {}
+    }
+
+private:
+    bool claim(uint64_t gen, unsigned& k) {
+        uint64_t v = ticket_.load(std::memory_order_acquire);
+        for (;;) {
+            if ((v >> 40) != gen || (v & 0xFFFFFu) >= ((v >> 20) & 0xFFFFFu)) return false;
+            if (ticket_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) {
+                k = (unsigned)(v & 0xFFFFFu);
+                return true;
+            }
+        }
+    }
+    void work(uint64_t gen) {
+        unsigned k;
+        while (claim(gen, k)) {
+            (*fn_.load(std::memory_order_relaxed))(k);
+            pending_.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const auto t0 = std::chrono::steady_clock::now();
+            uint64_t g;
+            unsigned spins = 0;
+            while ((g = ticket_.load(std::memory_order_acquire) >> 40) == seen) {
+                if ((++spins & 1023u) == 0 &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
+                    std::unique_lock<std::mutex> l(m_);
+                    sleepers_.fetch_add(1, std::memory_order_seq_cst);
+                    cv_.wait(l, [&] { return (ticket_.load(std::memory_order_seq_cst) >> 40) != seen; });
+                    sleepers_.fetch_sub(1, std::memory_order_relaxed);
+                }
+            }
+            seen = g;
+            work(g);
+        }
+    }
+    std::atomic<uint64_t> ticket_{0};
+    std::atomic<unsigned> pending_{0}, sleepers_{0};
+    std::atomic<const std::function<void(unsigned)>*> fn_{nullptr};
+    std::mutex submit_, m_;
+    std::condition_variable cv_;
+    long spin_us_ = 200;
+    unsigned workers_ = 0;
+};
+
+int g_host_pool = -1;  // workers; -1: PM_HOST_POOL (default 3)
+HostPool* host_pool() {
+    static std::mutex mu;
+    static HostPool* pool = nullptr;  // leaked: its detached workers outlive every object
+    std::lock_guard<std::mutex> g(mu);
+    if (g_host_pool < 0) g_host_pool = std::max(0, std::min(env_int("PM_HOST_POOL", 3), 15));
+    if (g_host_pool == 0) return nullptr;
+    if (!pool) pool = new HostPool((unsigned)g_host_pool);
+    return pool;
+}
+
+// f(lo, hi) over [0, n) of a small block: pieces on the pool, or the caller alone.
+template <class F>
+void small_par(size_t n, const F& f) {
+    HostPool* p = n >= ((size_t)16 << 10) ? host_pool() : nullptr;
+    const unsigned pieces = p ? std::min<unsigned>(p->workers() + 1, (unsigned)(n >> 14)) : 1u;
+    if (pieces <= 1) {
+        f((size_t)0, n);
+        return;
+    }
+    const size_t step = (n + pieces - 1) / pieces;
+    p->run(pieces, [&](unsigned k) {
+        const size_t lo = std::min(n, (size_t)k * step), hi = std::min(n, lo + step);
+        if (lo < hi) f(lo, hi);
+    });
+}
+
 // f(lo, hi) over [0, n) split across host threads, pieces of at least grain.
 template <class F>
 void par_range(size_t n, size_t grain, const F& f) {
@@ -570,21 +682,26 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         if (out_gid && q.staged && q.w == 2) {  // widen
             const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
             uint32_t* dst = out_gid + q.off;
-            for (size_t j = 0; j < q.m; ++j) dst[j] = g[j];
-        } else if (narrow) {
-            const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
-            pm_pattern_id_t* dst = out_ids + q.off;
-            par_range(q.m, (size_t)1 << 18, [&](size_t lo, size_t hi) {
-                for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
+            small_par(q.m, [&](size_t lo, size_t hi) {
+                for (size_t j = lo; j < hi; ++j) dst[j] = g[j];
             });
         } else if (!out_gid) {
-            const uint32_t* g = q.h_res;
             pm_pattern_id_t* dst = out_ids + q.off;
-            par_range(q.m, (size_t)1 << 18, [&](size_t lo, size_t hi) {
-                for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
-            });
+            auto map_ids = [&](size_t lo, size_t hi) {
+                if (narrow) {
+                    const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
+                    for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
+                } else {
+                    const uint32_t* g = q.h_res;
+                    for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
+                }
+            };
+            if (q.staged) small_par(q.m, map_ids);
+            else par_range(q.m, (size_t)1 << 18, map_ids);
         } else if (q.staged) {
-            std::memcpy(out_gid + q.off, q.h_res, q.m * sizeof(uint32_t));
+            small_par(q.m, [&](size_t lo, size_t hi) {
+                std::memcpy(out_gid + q.off + lo, q.h_res + lo, (hi - lo) * sizeof(uint32_t));
+            });
         }
         q.busy = false;
         lap(3);
@@ -1033,6 +1150,10 @@ void pm_hip_debug_rt_blocks(int b) { pm_rt_set_max_blocks(b); }
 void pm_hip_debug_rt_small(int64_t n) { pm_rt_set_small_max(n); }
 void pm_hip_debug_rt_small_stage(int on) { pm_rt_set_small_stage(on); }
 void pm_hip_debug_host_spin(int on) { g_host_spin = on < 0 ? -1 : on != 0; }
+void pm_hip_debug_host_pool(int workers) {
+    // a pool once made keeps its workers; 0 turns its use off, > 0 back on
+    g_host_pool = workers < 0 ? -1 : workers;
+}
 void pm_hip_debug_host_small(int gid16, int events) {
     g_gid16 = gid16 < 0 ? -1 : gid16 != 0;
     g_small_events = events < 0 ? -1 : events != 0;

@@ -8,7 +8,8 @@ and ac kinds, gids and pattern ids.  PM_HOST_VARIANTS (e.g.
 LDS text staging (pm_hip_debug_rt_small_stage) and the spin wait
 (pm_hip_debug_host_spin), u16 gids for small gid calls ("g16") and the
 per-call timing events ("ev": device_us is 0 without them,
-pm_hip_debug_host_small), side by side.  Prints one JSON object."""
+pm_hip_debug_host_small) and the host pool off ("pool0",
+pm_hip_debug_host_pool), side by side.  Prints one JSON object."""
 import ctypes
 import json
 import os
@@ -35,6 +36,7 @@ for var, kind in [(v, k) for v in (variants.split(",") if variants else [""])
         lib.pm_hip_debug_rt_small_stage(1 if "stage1" in var else 0)
         lib.pm_hip_debug_host_spin(1 if "spin" in var else 0)
         lib.pm_hip_debug_host_small(1 if "g16" in var else 0, 1 if "ev" in var else 0)
+        lib.pm_hip_debug_host_pool(0 if "pool0" in var else -1)
     m = pm.HipMatcher(kind)
     m.add_dictionary(d)
     m.compile()

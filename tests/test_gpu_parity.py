@@ -416,7 +416,9 @@ def test_small_gid_calls_u16_and_u32(kind, key):
     """Small read_block_gid calls (<= 256 Ki positions) bring u16 gids over
     the link and widen them on the host when every gid fits, u32 otherwise
     (a 70,000-pattern dictionary), with or without the per-call timing
-    events (pm_hip_debug_host_small): every form equals one large call."""
+    events (pm_hip_debug_host_small), their results copied / mapped on the
+    host pool or by the caller alone (pm_hip_debug_host_pool): every form
+    equals one large call, for gids and pattern ids."""
     lib = pm.load()
     if key == "snort":
         m = matcher("snort", kind)
@@ -432,14 +434,21 @@ def test_small_gid_calls_u16_and_u32(kind, key):
     whole = m.read_block_gids(text)  # > 256 Ki positions: u32 straight into the caller's array
     if key == "70k":
         assert whole.max() >= 65536
+    m.reset()
+    whole_ids = m.read_block_id_array(text)
     try:
-        for gid16, ev in ((1, 0), (0, 0), (1, 1)):
+        for gid16, ev, pool in ((1, 0, -1), (0, 0, -1), (1, 1, -1), (0, 1, 0), (1, 0, 0)):
             lib.pm_hip_debug_host_small(gid16, ev)
+            lib.pm_hip_debug_host_pool(pool)  # the result copy / id map on the host pool, or not
             m.reset()
             parts = [m.read_block_gids(text[o:o + (100 << 10)]) for o in range(0, len(text), 100 << 10)]
-            assert np.array_equal(np.concatenate(parts), whole), (gid16, ev)
+            assert np.array_equal(np.concatenate(parts), whole), (gid16, ev, pool)
+            m.reset()
+            ids = [m.read_block_id_array(text[o:o + (100 << 10)]) for o in range(0, len(text), 100 << 10)]
+            assert np.array_equal(np.concatenate(ids), whole_ids), (gid16, ev, pool)
     finally:
         lib.pm_hip_debug_host_small(-1, -1)
+        lib.pm_hip_debug_host_pool(-1)
     if key == "70k":
         m.free()
 
