@@ -918,7 +918,13 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             // table only for the other lanes -- by exec mask or with those
             // lanes on one broadcast address: exact, but 0.433 -> 0.647 /
             // 0.668 ms on ASCII, the 16 extra LDS reads per chunk cost more
-            // than the conflicts they remove; profiles/r04/count_ablations)
+            // than the conflicts they remove; profiles/r04/count_ablations.
+            // Also measured and removed: a u16 class table whose zero
+            // answers carry a filter of their depth-3 children's bytes (low
+            // 3 bits of text[i-2]), candidates 2.1% -> 0.5% of random-ASCII
+            // positions -- exact, but 0.444 -> 0.473 ms on ASCII, 0.600 ->
+            // 0.659 shipped, 0.841 -> 0.834 lines: the classification, not
+            // the candidates, is what count only waits for; count4_*.json)
 #pragma unroll
             for (int j = 0; j < 16; ++j) f |= (uint32_t)s_t8[RT_T8KEY(j)] << (2 * j);
 #undef RT_T8KEY
