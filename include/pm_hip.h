@@ -223,8 +223,9 @@ void pm_hip_debug_dfa_variant(int v);
  * timing ablations of 28 (no escape lookups / no stores / neither staging
  * nor stores; u32 ids only, wrong ids);
  * 34 = 28 with the u16 copy of the escape table (every gid < 65536),
- * 35 / 36 = u16 staging rows and 88 / 48 LDS rows (u32 ids; u16 ids run
- * 34); -1 = the product choice (35 for u32 ids, 28 when a gid exceeds u16,
+ * 35 / 36 = u16 staging rows, 88 / 48 LDS rows and non-temporal line
+ * stores, 37 = 35 with plain stores (u32 ids; u16 ids run 34); -1 = the
+ * product choice (35 for u32 ids, 28 when a gid exceeds u16,
  * 12 for u16, 10 for count only). */
 void pm_hip_debug_dfa_lds(int v);
 /* Timing experiments only: 0 = every warm-up of the sparse form's product

@@ -1913,7 +1913,7 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
 // sdfa_wave_model.cpp, lines stream: 1.91 dependent loads per wave step with
 // 16 rows, 1.77 with 80).  An escape's slot holds the low 16 bits of its
 // state, the high 4 bits sit in four registers (hi4, 8 positions each).
-template <int KR, int BU>
+template <int KR, int BU, bool NT = false>
 __global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
@@ -1995,7 +1995,10 @@ __global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
                     const uint32_t* src = wrows + c * SROW + 2 * (lane & 7);
                     const uint32_t w0 = src[0], w1 = src[1];
                     const tu32x4 v = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
-                    if ((am >> c) & 1u) *reinterpret_cast<tu32x4*>(o) = v;
+                    if ((am >> c) & 1u) {
+                        if (NT) __builtin_nontemporal_store(v, reinterpret_cast<tu32x4*>(o));
+                        else *reinterpret_cast<tu32x4*>(o) = v;
+                    }
                     o += 8 * seg_len;
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -2499,14 +2502,18 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             if (outw == 4) DST(4, 16, 1024, false); else DST(2, 16, 1024, false);
         } else if (sdfa_lds == 28) {  // 27 with 4-unit (32-B) record blocks
             if (outw == 4) DST4(4); else DST4(2);
-        } else if (sdfa_lds >= 35 && sdfa_lds <= 36 && outw == 4) {  // u16 staging rows, 88 / 48 LDS rows
+        } else if (sdfa_lds >= 35 && sdfa_lds <= 37 && outw == 4) {  // u16 staging rows, 88 / 48 LDS rows (37: plain stores)
             // (measured and removed: 64-B record blocks here, 5.60 -> 5.84
             // lines, 3.76 -> 4.12 shipped, 3.80 -> 4.79 ASCII; profiles/r04/gid_order/stage16_blocks64_ab.json)
             if (!t.sout8h) return hipErrorInvalidValue;
-#define DS16(K, B)                                                                                                  \
-    hipLaunchKernelGGL((dfa_sparse_stage16_kernel<K, B>), gs, bs, 0, s, text, stream_start, pos0, n,                   \
+#define DS16(K, B, N)                                                                                               \
+    hipLaunchKernelGGL((dfa_sparse_stage16_kernel<K, B, N>), gs, bs, 0, s, text, stream_start, pos0, n,                \
                        reinterpret_cast<uint32_t*>(out), count, t.sbase8, t.sF, t.sout8, t.sout8h, t.warm, seg, g3)
-            if (sdfa_lds == 35) DS16(88, 4); else DS16(48, 4);
+            // (35: non-temporal whole-line stores, the product -- against
+            // plain ones, 37: lines 5.58 -> 5.45 ms, shipped 3.76 -> 3.56,
+            // ASCII 3.78 -> 3.49; profiles/r04/gid_order/stage16_nt_ab.json.
+            // The output lines no longer evict table lines from L2.)
+            if (sdfa_lds == 35) DS16(88, 4, true); else if (sdfa_lds == 36) DS16(48, 4, true); else DS16(88, 4, false);
 #undef DS16
         } else if (sdfa_lds >= 34) {  // 28 with the u16 escape table (and 35 / 36 for u16 ids)
             if (!t.sout8h) return hipErrorInvalidValue;
@@ -2705,7 +2712,7 @@ void pm_dfa_set_block(int blk) {
     g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
 }
 void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 36 ? v : -1; }
+void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 37 ? v : -1; }
 bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
 bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
 void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }

@@ -814,7 +814,7 @@ def test_sparse_dfa_kernel_variants_agree(stream):
     lib.pm_hip_debug_dfa_sparse(1)
     try:
         for size, start in ((n, 0), (777, 4096), (100 << 10, 12345 & ~15), (5 << 20, 3 << 20)):
-            for form, lanes, sync in [(f, ln, y) for f in list(range(13)) + [25, 26, 27, 28, 34, 35, 36]
+            for form, lanes, sync in [(f, ln, y) for f in list(range(13)) + [25, 26, 27, 28, 34, 35, 36, 37]
                                       for ln in ((512, 1024, 1536) if f in (2, 8, 9, 10, 12, 25, 27, 28) else (0,))
                                       for y in ((0, 1) if f in (10, 11, 12, 25, 27, 28, 34, 35) else (0,))]:
                     lib.pm_hip_debug_dfa_lds(form)
