@@ -1953,8 +1953,11 @@ __global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
                 act[tt] = lo + BLK * (b0 + tt) + BLK <= hi;
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
-                    const tu32x4 w = act[tt] ? *reinterpret_cast<const tu32x4*>(text + lo + BLK * (b0 + tt) + 16 * q)
-                                             : tu32x4{0u, 0u, 0u, 0u};
+                    // (measured and removed: non-temporal text loads -- lines
+                    // 5.47 -> 5.74 ms, the next segment's warm-up re-reads
+                    // these lines; shipped 3.43 -> 3.13; stage16_nt_text_ab.json)
+                    const tu32x4* tp = reinterpret_cast<const tu32x4*>(text + lo + BLK * (b0 + tt) + 16 * q);
+                    const tu32x4 w = act[tt] ? *tp : tu32x4{0u, 0u, 0u, 0u};
                     WT[tt][4 * q] = w.x;
                     WT[tt][4 * q + 1] = w.y;
                     WT[tt][4 * q + 2] = w.z;
@@ -2513,7 +2516,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             // plain ones, 37: lines 5.58 -> 5.45 ms, shipped 3.76 -> 3.56,
             // ASCII 3.78 -> 3.49; profiles/r04/gid_order/stage16_nt_ab.json.
             // The output lines no longer evict table lines from L2.)
-            if (sdfa_lds == 35) DS16(88, 4, true); else if (sdfa_lds == 36) DS16(48, 4, true); else DS16(88, 4, false);
+            if (sdfa_lds == 35) DS16(88, 4, true);
+            else if (sdfa_lds == 36) DS16(48, 4, true);
+            else DS16(88, 4, false);
 #undef DS16
         } else if (sdfa_lds >= 34) {  // 28 with the u16 escape table (and 35 / 36 for u16 ids)
             if (!t.sout8h) return hipErrorInvalidValue;
