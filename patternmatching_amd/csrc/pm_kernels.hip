@@ -1557,6 +1557,9 @@ __device__ __forceinline__ uint4 pick4(const uint4 (&R)[4], uint32_t k) {
 // BU (RB = 8): units per register block -- 8 (64 B, four 16-B loads) or 4
 // (32 B, two loads; pm_pack_sparse8 keeps a two-unit record inside an
 // aligned 32-B block)
+// (measured and removed: the fallback rows' words read non-temporally, so
+// row lines -- 64 B of which a step uses 4 -- would leave L2 to the
+// records: lines 5.46 -> 8.80 ms; profiles/r04/gid_order/stage16_nt_rows_ab.json)
 template <int KR, int RB = 16, int BU = 8>
 __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ base, uint32_t F,
                                                   const uint32_t* __restrict__ s_rows, uint32_t s, uint32_t c,
