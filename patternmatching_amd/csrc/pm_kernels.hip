@@ -2462,7 +2462,12 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
     // one segment per lane and chain, none shorter than short_seg (above)
     const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds : outw == 4 ? (t.sout8h ? 35 : 28) : outw ? 12 : 10;
+    // (without 8-B units -- an automaton whose unit ids pass 2^20 -- the
+    // staged kernels cannot run: 12 / 10 then take the 16-B records)
+    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds
+                         : outw == 4        ? (t.sout8h ? 35 : t.sbase8 ? 28 : 12)
+                         : outw             ? 12
+                                            : 10;
     const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
     const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
     const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
