@@ -321,10 +321,13 @@ def main():
                                                                   prop.pci_device_id),
               "uuid": str(getattr(prop, "uuid", "")), "name": prop.name}
     devices = [my_dev]
+    my_dev["host"] = socket.gethostname()
     if use_dist:
         devices = [None] * world
         dist.all_gather_object(devices, my_dev)
-        if backend == "nccl" and len({d["pci_bus_id"] for d in devices}) != world:
+        # one GPU per rank: distinct (host, PCI bus id) pairs -- every node of
+        # a multi-node world has its own GPUs with the same bus ids
+        if backend == "nccl" and len({(d["host"], d["pci_bus_id"]) for d in devices}) != world:
             if rank == 0:
                 print(f"bench.py: ranks share GPUs under RCCL: {devices}", file=sys.stderr, flush=True)
             sys.exit(3)
@@ -483,16 +486,16 @@ def main():
     elapsed, kernel_ms = stats.tolist()
     total_matches = int(matches.item())
 
-    # the same kernel's streaming floor, live on this GPU: variant 2 of
-    # rt_scan_kernel runs the chunk loop's loads and stores with no lookups
-    # (its ids are not matches; `out` is not used after this)
+    # the same kernel's streaming floor, live on this GPU: rt_scan_kernel<2>
+    # runs the chunk loop's loads and stores with no lookups (its ids are
+    # not matches; `out` is not used after this)
     floor = None
     if rank == 0 and args.kernel == "rt" and pos0 == 0:
         fts = []
         for r in range(4):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            rc = lib.pm_hip_debug_scan_variant(m.obj, 2, text.data_ptr(), n, out_ptr, width, None, stream.cuda_stream)
+            rc = lib.pm_hip_streaming_floor_device(m.obj, text.data_ptr(), n, out_ptr, width, stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
             if rc != 0:
@@ -503,8 +506,8 @@ def main():
             fms = sorted(fts)[len(fts) // 2]
             floor = {"kernel_ms": round(fms, 4), "achieved": round(n * (1 + width) / (fms * 1e-3) / 1e9, 2),
                      "kernel_over_floor": round(kernel_ms / fms, 4),
-                     "what": "rt_scan_kernel variant 2 on this GPU: the same loads and stores, no lookups "
-                             "(pm_hip_debug_scan_variant); kernel_over_floor = kernel_ms / floor kernel_ms"}
+                     "what": "rt_scan_kernel<2> on this GPU: the same loads and stores, no lookups "
+                             "(pm_hip_streaming_floor_device); kernel_over_floor = kernel_ms / floor kernel_ms"}
 
     # the default run's extra lines: count-only on the same stream, and the
     # deep lines stream through the auto kind
@@ -630,10 +633,16 @@ def main():
 def other_configs(args, pm, lib, world, all_reduce, dist, text, out):
     """The other BASELINE.json configs on the same kernels, per rank, timed
     like the headline (max over ranks): C2 (et.dict, 64 MiB ASCII, dense
-    u32 ids), C5 (snort + et merged, 4 GiB ASCII: four 1 GiB launches per
-    step, dense u32) and the merged dictionary on the deep lines stream
-    through the auto kind.  The 1 GiB text and id buffers of the headline
-    are reused where they are large enough."""
+    u32 ids), C5 (snort + et merged, 4 GiB ASCII, dense u32: one 4 GiB
+    scan_device call per step, which the RT launcher runs as four 1 GiB
+    kernel launches -- its queue keeps 30-bit positions), the merged
+    dictionary on the deep lines stream through the auto kind, and the
+    reference's own published configuration (results.csv:2-4): snort + et
+    merged over its shipped Streams/dictionaries_generated.stream, tiled to
+    1 GiB, through the auto kind.  The 1 GiB text and id buffers of the
+    headline are reused where they are large enough.  `traffic` comes from
+    profiles/traffic.json when a PMC summary of that exact workload exists
+    (rocprofv3 --pmc of the equivalent single-workload bench run)."""
     import torch
     res = {}
     stream = torch.cuda.current_stream()
@@ -648,6 +657,11 @@ def other_configs(args, pm, lib, world, all_reduce, dist, text, out):
         o = out if nbytes <= out.numel() else torch.empty(nbytes, dtype=torch.int32, device="cuda")
         if stream_kind == "lines":
             m.gen_lines_device(t.data_ptr(), nbytes + 64, args.seed + rank, stream.cuda_stream)
+        elif stream_kind == "ship":
+            import numpy as np
+            ship = torch.from_numpy(np.fromfile(os.path.join(DATA, "dictionaries_generated.stream"), dtype=np.uint8))
+            reps = (nbytes + 64 + ship.numel() - 1) // ship.numel()
+            t[: nbytes + 64].copy_(ship.to("cuda").repeat(reps)[: nbytes + 64])
         elif lib.pm_hip_gen_stream_device(t.data_ptr(), 0, nbytes + 64, args.seed + rank, 0, stream.cuda_stream):
             raise RuntimeError(lib.pm_hip_last_error().decode())
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -675,6 +689,7 @@ def other_configs(args, pm, lib, world, all_reduce, dist, text, out):
         ms = all_reduce(torch.tensor([ms], dtype=torch.float64, device="cuda"), dist.ReduceOp.MAX).item()
         matches = all_reduce(cnt.clone(), dist.ReduceOp.SUM).item() // steps
         ach = nbytes * 5 / (ms * 1e-3) / 1e9
+        tr = load_traffic(f"{dict_key}-{stream_kind}-{nbytes}-dense-{kind}")
         res[name] = {"dict": dict_key, "stream": stream_kind, "bytes_per_gpu": nbytes, "mode": "dense",
                      "kernel": kind + ("" if kind == "rt" else f" (held: {CAND_NAME.get(held, str(held))})"),
                      "steps": steps, "kernel_ms": round(ms, 4),
@@ -682,13 +697,16 @@ def other_configs(args, pm, lib, world, all_reduce, dist, text, out):
                      "matches_per_step": int(matches),
                      "table_bytes": int(m.table_bytes),
                      "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes * 5}}
+                                  "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes * 5,
+                                  "traffic": tr["traffic_bytes"] if tr else None,
+                                  "traffic_source": tr["source"] if tr else None}}
         m.free()
         del t, o
 
     run("C2_et_64MiB", "et", "rt", "ascii", 64 << 20, 20)
     run("C5_merged_4GiB", "merged", "rt", "ascii", 4 << 30, 5)
     run("merged_lines_auto", "merged", "auto", "lines", min(args.bytes, 1 << 30), 5)
+    run("merged_ship_auto", "merged", "auto", "ship", min(args.bytes, 1 << 30), 5)
     return res
 
 

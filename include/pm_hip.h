@@ -166,8 +166,14 @@ int pm_hip_kernel_last(void* obj);
 /* DFA form of the last launch: 1 = dense rows, 2 = rows + 16-B records
  * (pm_flatten.h), 0 = the RT kernel ran. */
 int pm_hip_dfa_form_last(void* obj);
+/* The sparse form's kernel of the last launch that ran it ("sparse_kernel"
+ * option numbering: 1 fallback-linked, 2 u16-staged 8-B units, 3 u32-staged,
+ * 4 lock-step 8-B units, 5 lock-step 16-B records; 0 before any). */
+int pm_hip_sparse_kernel_last(void* obj);
 /* Seconds of device time of the scan kernels issued through read_block
- * since the last reset (hipEvent based). */
+ * since the last reset (hipEvent based); -1 when some of those launches were
+ * not timed (the "host_events" option off): the device time is then
+ * unmeasured, not zero. */
 double pm_hip_device_seconds(void* obj);
 /* Bytes per position the last read_block's device scans wrote: 2 (u16 gids,
  * dictionaries of < 65,536 patterns, pattern-id output) or 4; 0 before any. */
@@ -184,88 +190,39 @@ int pm_hip_device_count(void);
 /* hipSetDevice for C callers (the CLI's -g); 0 on success. */
 int pm_hip_set_device(int device);
 
-/* Timing-only ablation launches of the reverse-trie kernel (variant 0 =
- * product kernel, 1 = no depth>=3 stage, 2 = streaming only, 3 = product
- * kernel with one deep walk per lane after the chunk loop); out_width
- * 4 / 2 = u32 / u16 ids (d_out may be NULL: count only).  Outputs of
- * variants 1-2 are not match ids; variant 3's are. */
-int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out,
-                              int out_width, unsigned long long* d_count, void* hip_stream);
-/* Launch shape of the AC-DFA kernel for timing sweeps: segments in flight
- * (lanes) per CU; 0 restores the default. */
-void pm_hip_debug_dfa_shape(int lanes_per_cu);
-/* Timing sweeps only: the AC-DFA kernel's shortest segment (0 = default). */
-void pm_hip_debug_dfa_min_seg(int min_seg);
-/* Timing sweeps only: segments per lane of the output-coded AC-DFA kernel
- * (1 or 2; 0 = default). */
-void pm_hip_debug_dfa_chains(int chains);
-/* Timing sweeps only: the AC-DFA form of output-coded automata, 1 = sparse
- * (rows + 16-B default-transition records, pm_flatten.h), 0 = dense rows,
- * -1 = default. */
-void pm_hip_debug_dfa_sparse(int sparse);
-/* Timing sweeps only: positions per block of both AC-DFA kernels (16 or 32;
- * 0 = the defaults). */
-void pm_hip_debug_dfa_block(int blk);
-/* Timing experiments only: variant of the sparse AC-DFA kernel for u32 ids
- * (bit 0 non-temporal id stores, bit 1 non-temporal text loads, bit 2
- * escapes looked up in the step loop, bit 3 64-position blocks; 0 = product). */
-void pm_hip_debug_dfa_variant(int v);
-/* Timing experiments only: the sparse AC-DFA form's kernel: 0 = the plain
- * kernel, 1 = LDS rows + register record blocks, 2 = record blocks without
- * LDS rows, 3 / 4 = (1) with two segments per lane, 5 / 6 = (2) with two
- * segments per lane, 7 / 8 = (2) with 16-position blocks (8: registers
- * capped for 6 waves per SIMD), 9 = (2) over 8-B record units, 10 = (9)
- * with two blocks' text per load, 11 / 12 = (10) with 32 / 64 rows in LDS;
- * 22 / 23 / 24 = (12) without HBM id lines / escape lookups / id stores
- * (timing ablations: wrong ids); 25 / 26 = ids staged in LDS and stored as
- * whole lines (plain / non-temporal), 27 = 25 with 1024-lane workgroups and
- * 16 rows in LDS, 28 = 27 with 4-unit (32-B) record blocks, 29 / 30 / 31 =
- * timing ablations of 28 (no escape lookups / no stores / neither staging
- * nor stores; u32 ids only, wrong ids);
- * 34 = 28 with the u16 copy of the escape table (every gid < 65536),
- * 35 / 36 = u16 staging rows, 88 / 48 LDS rows and non-temporal line
- * stores, 37 = 35 with plain stores (u32 ids; u16 ids run 34); -1 = the
- * product choice (35 for u32 ids, 28 when a gid exceeds u16,
- * 12 for u16, 10 for count only). */
-void pm_hip_debug_dfa_lds(int v);
-/* Timing experiments only: 0 = every warm-up of the sparse form's product
- * kernels starts max_len - 1 bytes back; 1 = at the last synchronizing
- * 3-gram (one in no pattern) when there is one; -1 = the default. */
-void pm_hip_debug_dfa_sync(int on);
-/* Tests only: the reverse-trie kernel's spill region bound per wave, in
- * 1024-position chunks (>= 1; 0 = the default 16), so a small launch
- * resolves full regions many times. */
-void pm_hip_debug_spill_cap(int chunks);
-/* Timing sweeps only: at most b workgroups per reverse-trie launch (0 = one
- * per CU). */
-void pm_hip_debug_rt_blocks(int b);
-/* Timing sweeps / tests: reverse-trie launches of at most n positions use
- * the one-thread-per-position kernel (0 = never; < 0 = the default). */
-void pm_hip_debug_rt_small(int64_t n);
-/* Timing / tests: the one-thread-per-position kernel stages each
- * workgroup's text window in LDS before its walks (1) or reads the text
- * where it lies (0, the default). */
-void pm_hip_debug_rt_small_stage(int on);
-/* Timing only: read_block waits for its slots by polling the stream (1)
- * or with hipStreamSynchronize (0); -1 = the default (PM_HOST_SPIN, 0). */
-void pm_hip_debug_host_spin(int on);
-/* Timing / tests: small read_block_gid calls (<= 256 Ki positions) bring
- * u16 gids over the link and widen them on the host when every gid fits
- * (gid16 = 1) or u32 gids (0, the default); small calls of either API time
- * their launch with events for pm_hip_device_seconds (events = 1, the
- * default) or not (0: ~2 us faster per call, but pm_hip_device_seconds
- * then leaves small calls out).  -1 restores a default (PM_HOST_GID16,
- * PM_HOST_SMALL_EVENTS). */
-void pm_hip_debug_host_small(int gid16, int events);
-/* Timing / tests: small read_block calls copy / map their results on a
- * persistent pool of host workers (> 0; the pool, once made, keeps the
- * size it was made with) or on the calling thread alone (0); -1 = the
- * default (PM_HOST_POOL, 3). */
-void pm_hip_debug_host_pool(int workers);
-/* Timing only: the read_block host path's breakdown since the last call --
- * out5 = {staging s, enqueue s, wait s, result copy / map s, calls} -- then
- * reset and turn the accounting on (on != 0) or off. */
-void pm_hip_debug_host_profile(int on, double* out5);
+/* Per-object options (set before or after compile(); they change which
+ * product kernel or host path the object's launches take, never a result).
+ * Returns 0, or -1 for an unknown name or a value out of range.
+ *   "dfa_form"        ac / auto kinds: 0 = timed choice between the DFA's
+ *                     dense rows and sparse form (default), 1 = dense rows,
+ *                     2 = sparse form (the pick measures again)
+ *   "sparse_kernel"   the sparse form's kernel: 0 = the product choice per
+ *                     output width (default), 1 = fallback-linked form (u32
+ *                     ids), 2 = u16-staged 8-B units (u32 ids), 3 = u32-staged
+ *                     8-B units, 4 = lock-step 8-B units, 5 = lock-step 16-B
+ *                     records; a launch the object or width cannot run with
+ *                     the forced kernel fails (-3)
+ *   "dfa_sync"        1 = DFA warm-ups start at the last synchronizing 3-gram
+ *                     (default), 0 = max_len - 1 bytes back
+ *   "rt_small_max"    reverse-trie launches of at most this many positions
+ *                     run one thread per position (-1 = default 256 Ki,
+ *                     0 = never)
+ *   "spill_cap_chunks" the reverse-trie spill region per wave, 1,024-position
+ *                     chunks (1..16; 0 = default 16)
+ *   "host_spin" / "host_gid16" / "host_events" / "host_pool"
+ *                     read_block's host path (-1 = the environment's
+ *                     default, 0 / 1; csrc/pm_plugin.hip HostOpts) */
+int pm_hip_set_option(void* obj, const char* name, int64_t value);
+/* The reverse-trie kernel's streaming floor on this GPU: the same chunk
+ * loop's loads and stores with no lookups (its d_out values are not match
+ * ids) over d_text[0, n).  bench.py's live floor.  0 on success. */
+int pm_hip_streaming_floor_device(void* obj, const uint8_t* d_text, int64_t n, void* d_out, int out_width,
+                                  void* hip_stream);
+/* The read_block host path's breakdown since the last call -- out5 =
+ * {staging s, enqueue s, wait s, result copy / map s, calls} -- then reset
+ * and turn the accounting on (on != 0) or off.  Process-wide accounting;
+ * changes no result. */
+void pm_hip_host_profile(int on, double* out5);
 
 /* ---- 3. host-only table images (no device; used by the CPU test suite
  *         to check the flattener, and by DESIGN.md sizing) ------------ */

@@ -94,7 +94,7 @@ typedef struct {
 
 typedef struct {
     double wall_seconds;       /* read_block/read_char calls, CLOCK_MONOTONIC */
-    double device_seconds;     /* kernel time reported by the plugin (0 if n/a) */
+    double device_seconds;     /* kernel time reported by the plugin (0 if n/a, < 0 if not measured) */
     uint64_t bytes;
     uint64_t nonnull;
     size_t total_mem;

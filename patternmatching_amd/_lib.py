@@ -109,23 +109,9 @@ SIGNATURES = {
     "pm_hip_last_error": (ctypes.c_char_p, []),
     "pm_hip_device_count": (ctypes.c_int, []),
     "pm_hip_set_device": (ctypes.c_int, [ctypes.c_int]),
-    "pm_hip_debug_scan_variant": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int64, c_vp, ctypes.c_int,
-                                                 c_vp, c_vp]),
-    "pm_hip_debug_dfa_shape": (None, [ctypes.c_int]),
-    "pm_hip_debug_dfa_min_seg": (None, [ctypes.c_int]),
-    "pm_hip_debug_dfa_chains": (None, [ctypes.c_int]),
-    "pm_hip_debug_dfa_sparse": (None, [ctypes.c_int]),
-    "pm_hip_debug_dfa_block": (None, [ctypes.c_int]),
-    "pm_hip_debug_dfa_variant": (None, [ctypes.c_int]),
-    "pm_hip_debug_dfa_lds": (None, [ctypes.c_int]),
-    "pm_hip_debug_dfa_sync": (None, [ctypes.c_int]),
-    "pm_hip_debug_spill_cap": (None, [ctypes.c_int]),
-    "pm_hip_debug_rt_blocks": (None, [ctypes.c_int]),
-    "pm_hip_debug_rt_small": (None, [ctypes.c_int64]),
-    "pm_hip_debug_rt_small_stage": (None, [ctypes.c_int]),
-    "pm_hip_debug_host_spin": (None, [ctypes.c_int]),
-    "pm_hip_debug_host_small": (None, [ctypes.c_int, ctypes.c_int]),
-    "pm_hip_debug_host_pool": (None, [ctypes.c_int]),
+    "pm_hip_set_option": (ctypes.c_int, [c_vp, ctypes.c_char_p, ctypes.c_int64]),
+    "pm_hip_streaming_floor_device": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, c_vp, ctypes.c_int, c_vp]),
+    "pm_hip_sparse_kernel_last": (ctypes.c_int, [c_vp]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),
     "pm_flat_build_cached": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int,
@@ -140,7 +126,7 @@ SIGNATURES = {
     "pm_hip_hbm_peak_gbs": (ctypes.c_double, []),
     "pm_hip_hold_choice": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "pm_hip_prepare_capture": (ctypes.c_int, [c_vp]),
-    "pm_hip_debug_host_profile": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
+    "pm_hip_host_profile": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "pm_hip_scratch_bytes": (ctypes.c_size_t, [c_vp]),
     "pm_flat_host_scan": (ctypes.c_int, [c_vp, c_u8p, ctypes.c_size_t, c_u32p, ctypes.c_int]),
 }
@@ -168,7 +154,7 @@ def load():
                            "(or __graft_entry__.build()); there is no CPU fallback")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        if not hasattr(lib, name) and (name.startswith("pm_hip_debug_") or os.environ.get("PM_LIBPM")):
+        if not hasattr(lib, name) and os.environ.get("PM_LIBPM"):
             continue  # an older build under A/B comparison (PM_LIBPM) may lack a newer entry point
         fn = getattr(lib, name)
         fn.restype = res

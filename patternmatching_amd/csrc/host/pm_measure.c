@@ -236,7 +236,13 @@ int pm_measure_all(PmConf* conf, PmDict* dict, PmInstanceStats* stats) {
                 if (got < chunk) break;
             }
             close(fd);
-            st->device_seconds += pm_hip_device_seconds(inst[a].obj);
+            {
+                /* < 0: some launches were not timed (pm_hip_set_option
+                 * "host_events" 0) -- the device columns are then unmeasured */
+                const double ds = pm_hip_device_seconds(inst[a].obj);
+                if (ds < 0 || st->device_seconds < 0) st->device_seconds = -1.0;
+                else st->device_seconds += ds;
+            }
             st->out_width = pm_hip_last_out_width(inst[a].obj);
         }
         st->total_mem = e->total_mem(inst[a].obj);
@@ -285,11 +291,17 @@ int pm_write_stats(const PmConf* conf, const PmInstanceStats* stats) {
          * device time, against the HBM peak bench.py uses too */
         const double dev_gbs = s->device_seconds > 0 ? (double)s->bytes / s->device_seconds / 1e9 : 0.0;
         const double per_pos = 1.0 + (s->out_width ? s->out_width : 4);
-        snprintf(buf, sizeof(buf), "\n%s,%.6f,%zu,%.6Lf,%.6Lf,%.6Lf,%.6f,%.3f,%llu,%llu,%.6g,%d", pm_mps_table[a].name,
+        /* device columns: empty when the device time was not measured */
+        char dt[32] = "", dg[32] = "", df[32] = "";
+        if (s->device_seconds >= 0) {
+            snprintf(dt, sizeof(dt), "%.6f", s->device_seconds);
+            snprintf(dg, sizeof(dg), "%.3f", dev_gbs);
+            snprintf(df, sizeof(df), "%.6g", dev_gbs * per_pos / PM_HBM_PEAK_GBS);
+        }
+        snprintf(buf, sizeof(buf), "\n%s,%.6f,%zu,%.6Lf,%.6Lf,%.6Lf,%s,%s,%llu,%llu,%s,%d", pm_mps_table[a].name,
                  s->wall_seconds, s->total_mem, (long double)s->sr.false_pos / den,
-                 (long double)s->sr.false_neg / den, (long double)s->sr.partial_suc / den, s->device_seconds, dev_gbs,
-                 (unsigned long long)s->nonnull, (unsigned long long)s->bytes, dev_gbs * per_pos / PM_HBM_PEAK_GBS,
-                 conf->device);
+                 (long double)s->sr.false_neg / den, (long double)s->sr.partial_suc / den, dt, dg,
+                 (unsigned long long)s->nonnull, (unsigned long long)s->bytes, df, conf->device);
         put(fd, buf);
     }
     put(fd, "\n");

@@ -537,6 +537,105 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
     return true;
 }
 
+bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
+    const uint32_t F = d.sF, S = d.states;
+    fl = FlImage();
+    if (d.sblock.empty() || F < 1 || F >= 65536) return false;
+    const uint32_t* rec = d.sblock.data() + (size_t)F * 256;
+    auto R = [&](uint32_t v) { return rec + (size_t)(v - F) * 4; };  // {x, y, z, w} of record v
+    for (uint32_t v = 0; v < S; ++v)
+        if (d.sout[v] >= 65536) return false;
+    // rows by fallback use (the root first: the warm-ups start there)
+    std::vector<uint64_t> use(F, 0);
+    for (uint32_t v = F; v < S; ++v) use[R(v)[3]]++;
+    std::vector<uint32_t> ord(F), nrow(F);
+    for (uint32_t r = 0; r < F; ++r) ord[r] = r;
+    std::stable_sort(ord.begin() + 1, ord.end(), [&](uint32_t a, uint32_t b) { return use[a] > use[b]; });
+    for (uint32_t k = 0; k < F; ++k) nrow[ord[k]] = k;
+    // folded slotless records; granules of the others
+    std::vector<uint8_t> fold(S, 0);
+    std::vector<uint32_t> gid(S, 0);  // granule of a record
+    uint64_t u = 0;
+    for (uint32_t v = F; v < S; ++v) {
+        const uint32_t* r = R(v);
+        const bool s0 = r[0] & 0x100u, s1 = r[0] & 0x1000000u;
+        if (!s0 && d.sout[v] < PM_DFA_ESC) {
+            fold[v] = 1;
+            ++fl.folded;
+            continue;
+        }
+        const bool wide = s1 || nrow[r[3]] >= PM_FL_FB_INREC;
+        if (wide && (u & 3) == 3) ++u;  // 16 B inside one aligned 32-B block
+        gid[v] = (uint32_t)u;
+        u += wide ? 2 : 1;
+        if (F + u > PM_DFA_STATE_MASK + 1) return false;
+    }
+    fl.F = F;
+    fl.granules = (uint32_t)u;
+    // the word into old state t
+    auto enc = [&](uint32_t t) -> uint32_t {
+        if (t < F) return nrow[t] | std::min(d.sout[t], PM_DFA_ESC) << 20;
+        const uint32_t* r = R(t);
+        if (fold[t]) return nrow[r[3]] | d.sout[t] << 20;
+        const bool s0 = r[0] & 0x100u, s1 = r[0] & 0x1000000u;
+        const bool chain = (s0 && (r[1] & PM_DFA_STATE_MASK) == t + 1) || (s1 && (r[2] & PM_DFA_STATE_MASK) == t + 1);
+        const uint32_t fb = std::min(nrow[r[3]], PM_FL_FB_INREC);
+        return (F + gid[t]) | ((chain ? 0u : 1u) << 11 | fb) << 20;
+    };
+    fl.block.assign((size_t)F * 256 + 2 * (size_t)u, 0);
+    fl.rowout16.assign(F, 0);
+    for (uint32_t r = 0; r < F; ++r) {
+        fl.rowout16[nrow[r]] = (uint16_t)d.sout[r];
+        const uint32_t* src = d.sblock.data() + (size_t)r * 256;
+        uint32_t* dst = fl.block.data() + (size_t)nrow[r] * 256;
+        for (uint32_t c = 0; c < 256; ++c) dst[c] = enc(src[c] & PM_DFA_STATE_MASK);
+    }
+    for (uint32_t v = F; v < S; ++v) {
+        if (fold[v]) continue;
+        const uint32_t* r = R(v);
+        uint32_t* U = fl.block.data() + (size_t)F * 256 + 2 * (size_t)gid[v];
+        const bool s0 = r[0] & 0x100u, s1 = r[0] & 0x1000000u;
+        uint32_t c0, c1, t0, t1;
+        if (!s0) {  // slotless (output escapes): one slot repeating the fallback's byte-0 transition
+            c0 = c1 = 0;
+            t0 = t1 = enc(d.sblock[(size_t)r[3] * 256] & PM_DFA_STATE_MASK);
+        } else {
+            c0 = r[0] & 0xFFu;
+            c1 = s1 ? (r[0] >> 16) & 0xFFu : c0;
+            t0 = enc(r[1] & PM_DFA_STATE_MASK);
+            t1 = s1 ? enc(r[2] & PM_DFA_STATE_MASK) : t0;
+        }
+        U[0] = d.sout[v] | c0 << 16 | c1 << 24;
+        U[1] = t0;
+        if (s1 || nrow[r[3]] >= PM_FL_FB_INREC) {
+            U[2] = t1;
+            U[3] = nrow[r[3]];
+        }
+    }
+    return true;
+}
+
+uint32_t pm_fl_output(const FlImage& fl, uint32_t w) {
+    const uint32_t s = w & PM_DFA_STATE_MASK;
+    if (s < fl.F) {
+        const uint32_t f = w >> 20;
+        return f < PM_DFA_ESC ? f : fl.rowout16[s];
+    }
+    return fl.block[(size_t)fl.F * 256 + 2 * (size_t)(s - fl.F)] & 0xFFFFu;
+}
+
+uint32_t pm_fl_host_step(const FlImage& fl, uint32_t w, uint8_t c, uint32_t* out_prev) {
+    const uint32_t s = w & PM_DFA_STATE_MASK;
+    if (out_prev) *out_prev = pm_fl_output(fl, w);
+    if (s < fl.F) return fl.block[(size_t)s * 256 + c];
+    const uint32_t* U = fl.block.data() + (size_t)fl.F * 256 + 2 * (size_t)(s - fl.F);
+    if (c == ((U[0] >> 16) & 0xFFu)) return U[1];
+    if (c == U[0] >> 24) return U[2];
+    const uint32_t fb = (w >> 20) & PM_FL_FB_INREC;
+    const uint32_t row = fb == PM_FL_FB_INREC ? U[3] : fb;
+    return fl.block[(size_t)row * 256 + c];
+}
+
 DfaImage pm_build_dfa(const std::vector<std::string>& pats, const PmGidMap& g) {
     DfaImage im;
     BfsTrie t = build_trie(pats, g, /*reversed=*/false, PM_DFA_DFS_DEPTH);

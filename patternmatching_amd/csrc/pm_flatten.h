@@ -164,6 +164,56 @@ PmParents pm_build_parents(const std::vector<std::string>& pats, const PmGidMap&
 // the coded word's 20-bit target field.
 bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vector<uint32_t>& out8);
 
+// The fallback-linked ("FL") form of the same automaton (round 5; a device
+// layout built from the 16-B form at compile, not cached).  In the 8-B form
+// a record's fallback row is inside the record, so a lane that enters a
+// record in a block it does not hold waits for the block and then, at a
+// slot miss, for the fallback row's word: two dependent loads, and with 64
+// lanes in lock step nearly every wave step waits for some lane's pair.
+// Here the word that leads INTO a record names its fallback row, so the
+// block and the row word can be loaded together.
+//   Rows [0, F): renumbered by how many records fall back to them (the root
+//   stays 0), so the fallback rows records use most have the smallest ids
+//   (and the first ones are the rows the kernel stages in LDS).
+//   Records: in the trie's order, at 8-B granules (state id = F + granule):
+//     word0 = out16 | c0 << 16 | c1 << 24   out16 = the record's OWN output
+//             (gid < 65536); c1 == c0 for one slot (a slotless record that
+//             cannot be folded, below, takes one slot repeating its
+//             fallback's transition on byte 0)
+//     word1 = the word on c0
+//     16-B records (two slots, or a fallback outside the word's range):
+//     word2 = the word on c1 (word1 again for one slot), word3 = the
+//             fallback row; never straddling an aligned 32-B block.
+//   A word (in rows and records): target | f << 20 with
+//     target a row: f = min(output of the target, PM_DFA_ESC) (escapes:
+//       FlImage::rowout16[target]);
+//     target a record: f = spec << 11 | fb, fb = its fallback row when that
+//       is < PM_FL_FB_INREC, else PM_FL_FB_INREC (the fallback is word3);
+//       spec = 1 when the record is not a chain interior (no slot to the
+//       next record), i.e. when a miss is likely: the kernel then loads the
+//       fallback row's word together with the record's block.
+//   The output of a position whose state is a record is that record's out16
+//   (read with the record at the next step); of a row state, the word's f.
+//   A slotless record whose output has an inline code is folded: every word
+//   into it names its fallback row instead (with its output as the code) --
+//   the same transitions, the same outputs.
+// False when it does not apply: 65,536 patterns or rows or more, or ids past
+// the 20-bit target field.
+constexpr uint32_t PM_FL_FB_INREC = 2047;
+struct FlImage {
+    std::vector<uint32_t> block;     // F * 256 row words, then 2 words per granule
+    std::vector<uint16_t> rowout16;  // output of each row (escapes)
+    uint32_t F = 0, granules = 0, folded = 0;
+};
+bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl);
+// One FL step from state s with the word w that led to it (w = 0 at the
+// root) on byte c: returns the next word.  *out_prev = the output of the
+// position whose step produced w (s's own output when s is a record; w's
+// code -- or the escaped row output -- when a row).  Host reference of the
+// device kernel (tests; pm_flat_host_scan mode 2).
+uint32_t pm_fl_host_step(const FlImage& fl, uint32_t w, uint8_t c, uint32_t* out_prev);
+uint32_t pm_fl_output(const FlImage& fl, uint32_t w);  // the output of the position whose step produced w
+
 // Compiled-image cache: the flattened tables of a
 // dictionary, on disk, keyed by a hash of the patterns in add order and the
 // image kind.  pm_image_key hashes (format version, kind, the layout

@@ -18,18 +18,30 @@ struct RtDev {
     unsigned long long* spill_total;  // when set: += items spilled (the auto kernel choice)
     uint32_t t3h_bits;
     uint32_t back;         // max pattern length - 1: the bytes a walk may read before its position
+    // per-object options (pm_hip_set_option): launches of at most small_max
+    // positions run the one-thread-per-position kernel (-1: the default,
+    // 256 Ki; 0: never); the spill region per wave in 1,024-position chunks
+    // (0: the default 16; smaller: tests resolve full regions many times)
+    int64_t small_max = -1;
+    int64_t spill_cap_chunks = 0;
 };
 
 // Spill items (8 B each) an RT launch over n positions needs in
-// RtDev::spill: one per position of each wave's chunks.  Launches of any n reuse one buffer of
+// RtDev::spill: one per position of each wave's chunks, up to the per-wave
+// cap (RtDev::spill_cap_chunks).  Launches of any n reuse one buffer of
 // this size for n' <= n.
-int64_t pm_rt_spill_items(int64_t n, int num_cu);
-// Tests: the spill region's bound per wave in chunks (>= 1; 0 restores the
-// default), so small launches resolve full regions many times.
-void pm_rt_set_spill_cap(int chunks);
-void pm_rt_set_max_blocks(int b);  // timing sweeps: RT workgroups per launch (0 = one per CU)
-void pm_rt_set_small_stage(int on);  // timing: rt_small_kernel stages its text window in LDS (default 0)
-void pm_rt_set_small_max(int64_t n);  // launches of <= n positions use rt_small_kernel (0 = never, < 0 = default)
+int64_t pm_rt_spill_items(int64_t n, int num_cu, int64_t cap_chunks);
+
+// Kernels of the sparse DFA form (DfaDev::sparse_kernel; pm_kernels.hip
+// pm_launch_dfa lists the product choice per output width)
+enum PmSparseKernel {
+    PM_SK_PRODUCT = 0,
+    PM_SK_FL = 1,       // dfa_fl_kernel: the fallback-linked form (u32 ids)
+    PM_SK_STAGE16 = 2,  // dfa_sparse_stage16_kernel: 8-B units, u16-staged ids (u32 ids)
+    PM_SK_STAGE = 3,    // dfa_sparse_stage_kernel: 8-B units, u32-staged ids
+    PM_SK_LOCK8 = 4,    // dfa_sparse_lds_kernel over 8-B units, lock step
+    PM_SK_LOCK16 = 5,   // dfa_sparse_lds_kernel over the 16-B records, lock step
+};
 
 struct DfaDev {
     const uint32_t* next;  // states * 256 (output-coded when coded, pm_flatten.h)
@@ -49,7 +61,14 @@ struct DfaDev {
     // can start at the last one before the segment instead of max_len - 1
     // bytes back.
     const uint32_t* gram3;
-    int form;              // 0 = the default (pm_dfa_set_sparse), 1 = dense rows, 2 = sparse
+    int form;              // 0 = the default (the sparse form when there is one), 1 = dense rows, 2 = sparse
+    int sync = 1;          // warm-ups from the last synchronizing 3-gram (0: max_len - 1 bytes back)
+    int sparse_kernel = PM_SK_PRODUCT;
+    // the fallback-linked form (pm_pack_sparse_fl), or null: the product
+    // kernel of the sparse form for u32 ids
+    const uint8_t* flbase;
+    const uint16_t* flrowout16;
+    uint32_t flF;
 };
 
 // Positions [pos0, pos0+n) of text; bytes back to stream_start are context.
@@ -57,28 +76,18 @@ struct DfaDev {
 // gids, valid when every gid < 65536), or null; count (u64) may be null.
 hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                         unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s);
-// ablation variants of the RT kernel (timing only; see pm_kernels.hip)
-hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
-                                void* out, int outw, unsigned long long* count, const RtDev& t, int num_cu,
-                                hipStream_t s);
+// The RT kernel's streaming floor (rt_scan_kernel<2>: the chunk loop's loads
+// and stores, no lookups; its ids are not matches) over text[0, n).
+hipError_t pm_launch_rt_floor(const uint8_t* text, int64_t n, void* out, int outw, const RtDev& t, int num_cu,
+                              hipStream_t s);
+// The DFA form DfaDev::form names (0: the sparse one when the automaton has
+// it), and for the sparse form DfaDev::sparse_kernel (0: the product choice).
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s);
-// launch shape of the DFA kernel (timing sweeps): lanes per CU; <= 0
-// restores the default
-void pm_dfa_set_shape(int lanes_per_cu);
-void pm_dfa_set_chains(int chains);
-void pm_dfa_set_min_seg(int min_seg);
-// Timing sweeps: force the form of coded automata (1 = sparse, 0 = dense
-// rows) for launches whose DfaDev::form is 0; < 0 = no forced form (the
-// default form is then the sparse one).
-void pm_dfa_set_sparse(int sparse);
-bool pm_dfa_forced_form();
-void pm_dfa_set_variant(int v);  // timing experiments of the sparse kernel (u32 ids, one chain)
-void pm_dfa_set_block(int blk);  // sparse form, one chain: positions per block (16 or 32)
-// sparse form's kernel (timing; pm_hip_debug_dfa_lds)
-void pm_dfa_set_lds(int v);
-void pm_dfa_set_sync(int on);  // warm-ups from synchronizing 3-grams (timing; default on)
-bool pm_dfa_default_sparse();  // the form a launch with DfaDev::form 0 runs
+// The sparse kernel (PmSparseKernel) a launch of this width runs, 0 when
+// it runs dense rows: the forced DfaDev::sparse_kernel where the object
+// and width allow it, else the product choice.
+int pm_dfa_sparse_choice(const DfaDev& t, int outw);
 // counts[0..4] += success, partial, false_neg, false_pos, all_matches of algo
 // against real (n u32 gids each, 16-B aligned); parent/depth: PmParents.
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,

@@ -509,9 +509,11 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     // as one byte per key, t8 = nz | cand << 1 (64 KiB, derived from t12
     // while staging), at LDS address 0: the 16-bit key (text[i] << 8 |
     // text[i-1]) is the byte address, one ds_read_u8, no base add or mask.
-    // (V = 13 / 14, count-only timing ablations: 13 drops the candidates
-    // after classification, 14 pushes them but skips the tail; wrong counts)
-    constexpr bool kT8 = (V == 0 || V == 13 || V == 14 || V == 15) && OUTW == 0;
+    // V: 0 = the product kernel, 2 = its streaming floor (the chunk loop's
+    // loads and stores, no lookups: bench.py's live floor; its ids are not
+    // matches).  Round-4 and earlier ablation variants are in git history.
+    static_assert(V == 0 || V == 2, "product kernel (0) or streaming floor (2)");
+    constexpr bool kT8 = V == 0 && OUTW == 0;
     constexpr int kLdsWords = kT8 ? RT_T2_U16 / 4 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP
                                   : RT_FILTER_WORDS + RT_T2_U16 / 2 + RT_F2_WORDS + 2 * RT_WAVES * RT_QCAP;
     __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsWords];
@@ -549,10 +551,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     }
     __syncthreads();
 
-    // ablation phase switches (V = 0: all on; V = 3: product kernel with
-    // the plain one-walk-per-lane tail, a cross-check of rt_tail; V = 6:
-    // no tail at all, V = 7: the tail's probe phase only; both timing only)
-    constexpr bool kFilter = V == 0 || V >= 3;
+    constexpr bool kFilter = V == 0;
     // Stage 2 at push time: only its passers are queued, so rounds are ~3.3x
     // rarer and all their candidates probe.  Rounds in the chunk loop, or
     // every candidate to the spill region for the tail.  Side by side
@@ -567,15 +566,14 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
     //         V10 (no rounds, stage 2 in the tail's batched probe phase)
     //         0.733 / 0.832 / 8.63 (V9 on the same box 0.763 / 0.879 / 7.95)
     // So the product: u32 = V8, count = V10, u16 = issue-time stage 2.
-    // (V = 15, count only: stage 2 at push time too, so only its passers
-    // go to the spill region)
-    constexpr bool kPushS2 = V == 8 || V == 9 || (V == 0 && OUTW == 4) || (V == 15 && OUTW == 0);
-    constexpr bool kRounds = !(V == 9 || V == 10 || ((V == 0 || V == 12 || V == 13 || V == 14 || V == 15) && OUTW == 0));
+    // (Count only with stage 2 at push time too measured slower: 0.440 ->
+    // 0.473 ms, profiles/r04/count_ablations.)
+    constexpr bool kPushS2 = V == 0 && OUTW == 4;
+    constexpr bool kRounds = !(V == 0 && OUTW == 0);
     // the stage-1 LDS filter; count-only without it (V = 0) queues every
     // zero-placeholder position under a depth-2 node with children (2.3%
     // of random-ASCII positions on snort) for the tail's batched stage 2
-    // (V = 12 keeps it, timing)
-    constexpr bool kStage1 = !((V == 0 || V == 13 || V == 14 || V == 15) && OUTW == 0);
+    constexpr bool kStage1 = !(V == 0 && OUTW == 0);
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: the compiler then knows every per-chunk
     // quantity below is wave-uniform (scalar loop, no exec-mask loop)
@@ -847,23 +845,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
         // every placeholder and spill store of this wave complete before
         // its walks patch or read them
         __builtin_amdgcn_s_waitcnt(0);
-        if (V == 6 || V == 14) {
-            cnt += sn;  // timing only: the chunk loop without the deep walks
-        } else if (V == 3) {
-            for (uint32_t k = lane; k < sn; k += 64) {
-                const uint32_t item = sp[2 * k + 1];
-                const int64_t i = pos0 + (int64_t)(item & RT_POSMASK);
-                const uint32_t v = rt_one(text, s_t, t, i, stream_start);
-                cnt += (uint32_t)(v != 0u) - (item >> 31);
-                if (OUTW) put_id<OUTW>(out, (int64_t)(item & RT_POSMASK), v);
-            }
-        } else if (V == 7) {
-            rt_tail<OUTW, true>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
-        } else if (V == 4) {
-            rt_tail<OUTW, false, 8>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
-        } else if (V == 5) {
-            rt_tail<OUTW, false, 6>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
-        } else {
+        {
             const uint32_t nwalk = rt_tail<OUTW>(text, stream_start, pos0, out, t, s_f2, sp, sn, lane, cnt);
             if (!kRounds && t.spill_total && nwalk && lane == 0)
                 atomicAdd(t.spill_total, (unsigned long long)nwalk);
@@ -929,7 +911,7 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
             for (int j = 0; j < 16; ++j) f |= (uint32_t)s_t8[RT_T8KEY(j)] << (2 * j);
 #undef RT_T8KEY
             cnt += (uint32_t)__popc(f & 0x55555555u);
-            cm = V == 13 ? 0u : f & 0xAAAAAAAAu;
+            cm = f & 0xAAAAAAAAu;
         } else {
 #pragma unroll
         for (int j = 0; j < 16; ++j) res[j] = V == 2 ? RT_KEY(j) & 0xFFFFu : s_t[RT_KEY(j) >> 8];
@@ -1118,54 +1100,31 @@ __global__ __launch_bounds__(RT_THREADS) void rt_scan_kernel(const uint8_t* __re
 // stage, no chunk loop, no queue; a launch costs about one walk's chain of
 // dependent loads.  CONT positions (depth-2 node with children) count
 // towards spill_total, the auto kind's deep-input signal.
-// STAGE (an option, pm_rt_set_small_stage): the workgroup first copies its
-// text window -- its 256 positions and the RtDev::back bytes before them --
-// into LDS with dword loads issued together, and the walks read it there.
-// Meant for read_block's zero-copy calls, whose `text` is the pinned host
-// staging buffer, where each dependent byte read of a walk is a round trip
-// over the link; measured no faster there (the writes over the link, not
-// the reads, are what the call waits for).  Needs back <= RT_SMALL_BACK_MAX
-// and a 4-B aligned `text`.
+// The deep-input signal of the auto kind (RtDev::spill_total) counts, like
+// the chunked kernel's spilled items, the positions that pass both LDS
+// filter stages -- the ones with a depth-3 probe to make -- not every
+// position under a depth-2 node with children (the unfiltered
+// count sent small launches to the DFA trials more often).
+// (Measured and removed, round 4: staging each workgroup's text window in
+// LDS first -- no faster at read_block's 100 KiB zero-copy calls, 40.6
+// against 39.3 us per call, profiles/r04/host_path/small_call_variants_ab.json.)
 constexpr int RT_SMALL_THREADS = 256;
-constexpr int RT_SMALL_BACK_MAX = 512;  // the RT image's max_len <= 511 (pm_flatten.cpp)
-template <int OUTW, bool STAGE>
+template <int OUTW>
 __global__ __launch_bounds__(RT_SMALL_THREADS) void rt_small_kernel(const uint8_t* __restrict__ text,
                                                                     int64_t stream_start, int64_t pos0, int64_t n,
                                                                     void* __restrict__ out,
                                                                     unsigned long long* __restrict__ count, RtDev t) {
     const int64_t k = (int64_t)blockIdx.x * RT_SMALL_THREADS + threadIdx.x;
-    const uint8_t* tx = text;
-    if constexpr (STAGE) {
-        // window [lo, hi) of stream indices, staged from the 4-aligned word at or before lo
-        // (a walk that reaches a leaf at depth max_len reads the byte before
-        // it, unused: the window starts 4 bytes earlier, after one pad word,
-        // so every read stays inside s_win)
-        __shared__ uint32_t s_win[(RT_SMALL_THREADS + RT_SMALL_BACK_MAX + 32) / 4];
-        const int64_t i0 = pos0 + (int64_t)blockIdx.x * RT_SMALL_THREADS;
-        const int64_t lo = i0 - (int64_t)t.back - 4 > stream_start ? i0 - (int64_t)t.back - 4 : stream_start;
-        const int64_t hi = i0 + RT_SMALL_THREADS < pos0 + n ? i0 + RT_SMALL_THREADS : pos0 + n;
-        const int64_t w0 = lo >> 2;  // text is 4-B aligned: stream index 4w = word w
-        const uint32_t* tw = reinterpret_cast<const uint32_t*>(text);
-        for (int64_t w = w0 + threadIdx.x; 4 * w < hi; w += RT_SMALL_THREADS) {
-            uint32_t v;
-            if (4 * w >= lo && 4 * w + 4 <= hi) {
-                v = tw[w];
-            } else {  // a partial edge word: only bytes inside [lo, hi)
-                v = 0;
-                for (int b = 0; b < 4; ++b)
-                    if (4 * w + b >= lo && 4 * w + b < hi) v |= (uint32_t)text[4 * w + b] << (8 * b);
-            }
-            s_win[1 + w - w0] = v;
-        }
-        __syncthreads();
-        // a flat pointer whose [i] is s_win's byte of stream index i
-        tx = reinterpret_cast<const uint8_t*>(s_win + 1) - 4 * w0;
-    }
     uint32_t v = 0, deep = 0;
     if (k < n) {
         const int64_t i = pos0 + k;
-        v = rt_one(tx, t.t12, t, i, stream_start);
-        if (i - stream_start >= 2) deep = (t.t12[(uint32_t)tx[i] << 8 | tx[i - 1]] & CONT16) != 0;
+        v = rt_one(text, t.t12, t, i, stream_start);
+        if (t.spill_total && i - stream_start >= 3 && (t.t12[(uint32_t)text[i] << 8 | text[i - 1]] & CONT16)) {
+            const uint32_t q = (uint32_t)text[i - 3] | (uint32_t)text[i - 2] << 8 | (uint32_t)text[i - 1] << 16 |
+                               (uint32_t)text[i] << 24;
+            const uint32_t f = rt_fhash(q >> 8);
+            if (rt_fhit(t.filt[f >> 20], f)) deep = rt_stage2_hit(rt_stage2_load(t.filt + RT_FILTER_WORDS, q));
+        }
         if (OUTW) put_id<OUTW>(out, k, v);
     }
     const uint64_t nz = __ballot(v != 0u), dp = __ballot(deep != 0u);
@@ -1237,6 +1196,7 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
 // per lane).  Escapes are looked up after each 16-step block, off the chain.
 constexpr uint32_t DFA_STATE_MASK = 0xFFFFFu;  // must match pm_flatten.h
 constexpr uint32_t DFA_ESC = 4095u;
+constexpr uint32_t PM_FL_INREC = 2047u;  // must match pm_flatten.h PM_FL_FB_INREC
 
 // The start of the last synchronizing 3-gram in [wlo, lo - 3], or wlo when
 // there is none (DfaDev::gram3: no pattern holds it, so the state after it is
@@ -1362,172 +1322,16 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_coded_kernel(const uint8_t* _
     }
 }
 
-// Sparse (default-transition) DFA, pm_flatten.h: the same automaton with
-// rows only for the states whose row differs from their fallback's in more
-// than PM_SDFA_K bytes, 16-B records for the rest.  A step is one 16-B load
-// from one block (a row's aligned quad holding the byte, or the record) and,
-// at a record whose two slots miss the byte, one 4-B load of the fallback's
-// row.  On deep inputs the states a stream visits are mostly records: their
-// table is tens of MB instead of the dense rows' hundreds, so the loads stay
-// in L2 / the Infinity Cache instead of going to HBM.
-__device__ __forceinline__ uint32_t sdfa_off(uint32_t s, uint32_t c, uint32_t F) {
-    return s < F ? s * 1024u + (c & 0xFCu) * 4u : s * 16u + F * 1008u;  // F*1024 + (s-F)*16
-}
-
-template <int CH, bool kNoMiss = false>
-__device__ __forceinline__ void sdfa_step(const uint8_t* __restrict__ base, uint32_t F, const uint32_t (&s)[CH],
-                                          const uint32_t (&c)[CH], uint32_t (&v)[CH]) {
-    uint4 q[CH];
-#pragma unroll
-    for (int k = 0; k < CH; ++k) q[k] = *reinterpret_cast<const uint4*>(base + sdfa_off(s[k], c[k], F));
-    bool miss[CH];
-#pragma unroll
-    for (int k = 0; k < CH; ++k) {
-        const uint32_t key = c[k] | 0x100u;
-        const uint32_t rowv = (c[k] & 2u) ? ((c[k] & 1u) ? q[k].w : q[k].z) : ((c[k] & 1u) ? q[k].y : q[k].x);
-        const bool h0 = (q[k].x & 0x1FFu) == key, h1 = ((q[k].x >> 16) & 0x1FFu) == key;
-        const bool isrow = s[k] < F;
-        v[k] = isrow ? rowv : (h0 ? q[k].y : q[k].z);
-        miss[k] = !isrow && !h0 && !h1;
-    }
-    if (kNoMiss) {  // timing ablation only: a miss goes to the root (wrong ids, every state in range)
-#pragma unroll
-        for (int k = 0; k < CH; ++k) v[k] = miss[k] ? 0u : v[k];
-        return;
-    }
-#pragma unroll
-    for (int k = 0; k < CH; ++k)
-        if (miss[k]) v[k] = *reinterpret_cast<const uint32_t*>(base + q[k].w * 1024u + c[k] * 4u);
-}
-
-// VAR (timing experiments, pm_dfa_set_variant): bit 0 = non-temporal id
-// stores, bit 1 = non-temporal text loads, bit 2 = escape lookups issued in
-// the step loop (no per-position state registers), bit 3 = no second load
-// at a record miss (ablation: wrong ids, timing only), bit 4 = no escape
-// lookups (ablation: ids >= 4095 read as 4095, timing only)
-template <int OUTW, int CH, int BLK, int VAR = 0>
-__global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* __restrict__ text,
-                                                                 int64_t stream_start, int64_t pos0, int64_t n,
-                                                                 void* __restrict__ out,
-                                                                 unsigned long long* __restrict__ count,
-                                                                 const uint8_t* __restrict__ base, uint32_t F,
-                                                                 const uint32_t* __restrict__ outt, int64_t warm,
-                                                                 int64_t seg_len) {
-    const int64_t nseg = (n + seg_len - 1) / seg_len;
-    const int64_t lanes = (int64_t)gridDim.x * DFA_THREADS;
-    uint32_t cnt = 0;
-    for (int64_t sg0 = (int64_t)blockIdx.x * DFA_THREADS + threadIdx.x; sg0 < nseg; sg0 += CH * lanes) {
-        int64_t lo[CH], hi[CH], wlo[CH];
-        uint32_t s[CH];
-        int64_t wmax = 0;
-#pragma unroll
-        for (int k = 0; k < CH; ++k) {
-            const int64_t sg = sg0 + k * lanes;
-            lo[k] = sg < nseg ? pos0 + sg * seg_len : pos0 + n;
-            hi[k] = sg < nseg ? (lo[k] + seg_len < pos0 + n ? lo[k] + seg_len : pos0 + n) : pos0 + n;
-            wlo[k] = lo[k] - warm;
-            if (wlo[k] < stream_start) wlo[k] = stream_start;
-            if (sg >= nseg) wlo[k] = lo[k];
-            s[k] = 0;
-            wmax = lo[k] - wlo[k] > wmax ? lo[k] - wlo[k] : wmax;
-        }
-        // warm-up: every chain from the root, right-aligned so they end together
-        for (int64_t j = wmax; j > 0; --j) {
-            uint32_t c[CH], v[CH];
-#pragma unroll
-            for (int k = 0; k < CH; ++k) c[k] = lo[k] - j >= wlo[k] ? text[lo[k] - j] : 0u;
-            sdfa_step<CH>(base, F, s, c, v);
-#pragma unroll
-            for (int k = 0; k < CH; ++k) s[k] = lo[k] - j >= wlo[k] ? v[k] & DFA_STATE_MASK : s[k];
-        }
-        // blocks of BLK positions per chain: BLK / 16 16-B text loads, and
-        // the block's ids stored at once (BLK = 32: one whole 128-B line of
-        // u32 ids per lane, so the L2 never holds a half-written line)
-        constexpr int NW = BLK / 4;
-        const int64_t nblk = seg_len / BLK;
-        for (int64_t b = 0; b < nblk; ++b) {
-            bool act[CH];
-            uint32_t W[CH][NW];
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < CH; ++k) {
-                act[k] = lo[k] + BLK * b + BLK <= hi[k];
-                any |= act[k];
-#pragma unroll
-                for (int q = 0; q < BLK / 16; ++q) {
-                    using v4 = __attribute__((ext_vector_type(4))) unsigned int;
-                    const v4* tp = reinterpret_cast<const v4*>(text + lo[k] + BLK * b + 16 * q);
-                    const v4 w = act[k] ? ((VAR & 2) ? __builtin_nontemporal_load(tp) : *tp) : v4{0u, 0u, 0u, 0u};
-                    W[k][4 * q] = w.x; W[k][4 * q + 1] = w.y; W[k][4 * q + 2] = w.z; W[k][4 * q + 3] = w.w;
-                }
-            }
-            if (!any) break;
-            uint32_t code[CH][BLK], st[CH][BLK];
-#pragma unroll
-            for (int j = 0; j < BLK; ++j) {
-                uint32_t c[CH], v[CH];
-#pragma unroll
-                for (int k = 0; k < CH; ++k) c[k] = (W[k][j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                sdfa_step<CH, (VAR & 8) != 0>(base, F, s, c, v);
-#pragma unroll
-                for (int k = 0; k < CH; ++k) {
-                    s[k] = act[k] ? v[k] & DFA_STATE_MASK : s[k];
-                    code[k][j] = v[k] >> 20;
-                    if (VAR & 4) {
-                        if (code[k][j] == DFA_ESC) code[k][j] = outt[s[k]];
-                    } else {
-                        st[k][j] = s[k];
-                    }
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < CH; ++k) {
-                if (!act[k]) continue;
-                uint32_t r[BLK];
-#pragma unroll
-                for (int j = 0; j < BLK; ++j)
-                    r[j] = (VAR & 4) || (VAR & 16) || !OUTW ? code[k][j]
-                           : code[k][j] == DFA_ESC ? outt[st[k][j]] : code[k][j];
-                const int64_t i = lo[k] + BLK * b;
-                if (OUTW == 4) {
-                    using v4 = __attribute__((ext_vector_type(4))) unsigned int;
-                    v4* o = reinterpret_cast<v4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
-#pragma unroll
-                    for (int q = 0; q < BLK / 4; ++q) {
-                        const v4 x = {r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
-                        if (VAR & 1) __builtin_nontemporal_store(x, o + q);
-                        else o[q] = x;
-                    }
-                }
-                if (OUTW == 2) {
-                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + (i - pos0));
-#pragma unroll
-                    for (int q = 0; q < BLK / 8; ++q)
-                        o[q] = make_uint4(r[8 * q] | r[8 * q + 1] << 16, r[8 * q + 2] | r[8 * q + 3] << 16,
-                                          r[8 * q + 4] | r[8 * q + 5] << 16, r[8 * q + 6] | r[8 * q + 7] << 16);
-                }
-#pragma unroll
-                for (int j = 0; j < BLK; ++j) cnt += r[j] != 0u;
-            }
-        }
-        // the segments' last (< BLK) positions, one chain at a time
-#pragma unroll
-        for (int k = 0; k < CH; ++k) {
-            for (int64_t i = lo[k] + BLK * ((hi[k] - lo[k]) / BLK); i < hi[k]; ++i) {
-                uint32_t s1[1] = {s[k]}, c1[1] = {text[i]}, v1[1];
-                sdfa_step<1>(base, F, s1, c1, v1);
-                s[k] = v1[0] & DFA_STATE_MASK;
-                const uint32_t v = outt[s[k]];
-                if (OUTW) put_id<OUTW>(out, i - pos0, v);
-                cnt += v != 0u;
-            }
-        }
-    }
-    if (count) {
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
-        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
-    }
-}
+// The sparse (default-transition) form, pm_flatten.h: rows only for the
+// states whose row differs from their fallback's in more than PM_SDFA_K
+// bytes, 16-B records for the rest (8-B units in pm_pack_sparse8's
+// repacking).  A step reads a row's word, or the state's record and, at a
+// record whose slots miss the byte, the fallback row's word.  On deep
+// inputs the states a stream visits are mostly records: their table is tens
+// of MB instead of the dense rows' hundreds, so the loads stay in L2 / the
+// Infinity Cache instead of going to HBM.  (The round-2 kernel that loaded
+// each step's 16-B record or row quad, dfa_sparse_kernel, and its variants
+// are in git history before round 5.)
 
 // The sparse form with the transition tiles placed by the memory hierarchy
 // (one segment per lane; DFA_LDS_THREADS lanes per workgroup, one
@@ -1544,7 +1348,6 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_sparse_kernel(const uint8_t* 
 // Every other step is the plain form's: a 4-B load of a row word, or at a
 // record whose two slots miss the byte the fallback row's word.
 constexpr int DFA_LDS_THREADS = 512;
-constexpr int DFA_LDS_ROWS = 128;  // KiB of LDS: rows [0, 128)
 __device__ __forceinline__ uint4 pick4(const uint4 (&R)[4], uint32_t k) {
     const uint4 a = (k & 1u) ? R[1] : R[0], b = (k & 1u) ? R[3] : R[2];
     return (k & 2u) ? b : a;
@@ -1606,14 +1409,8 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
     return *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
 }
 
-// WPE: the waves per SIMD the register allocation must allow (0: the
-// compiler's choice); each more resident workgroup is 512 more chains per CU
-// TX: timing ablations of the id output (u32 ids; wrong ids): 3 = every
-// block's ids to one line per lane (stays in L2), 4 = no escape lookups,
-// 5 = no id stores (profiles/r04/dyn/store_escape_ablations.txt).
-template <int OUTW, int BLK, int KR, int CH = 1, int WPE = 0, int RB = 16, int TB = 1, int TX = 0>
-__global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
-void dfa_sparse_lds_kernel(
+template <int OUTW, int BLK, int KR, int CH = 1, int RB = 16, int TB = 1>
+__global__ __launch_bounds__(DFA_LDS_THREADS) void dfa_sparse_lds_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
     const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
@@ -1714,23 +1511,13 @@ void dfa_sparse_lds_kernel(
             for (int k = 0; k < CH; ++k) {
                 if (!act[k]) continue;
                 uint32_t r[BLK];
-                // (count only: an escape code is a nonzero id, no lookup;
-                // TX = 4, timing ablation: no escape lookups either)
+                // (count only: an escape code is a nonzero id, no lookup)
 #pragma unroll
                 for (int j = 0; j < BLK; ++j)
-                    r[j] = OUTW && TX != 4 && (vw[k][j] >> 20) == DFA_ESC ? outt[vw[k][j] & DFA_STATE_MASK]
-                                                                         : vw[k][j] >> 20;
+                    r[j] = OUTW && (vw[k][j] >> 20) == DFA_ESC ? outt[vw[k][j] & DFA_STATE_MASK] : vw[k][j] >> 20;
                 const int64_t i = lo[k] + BLK * b;
-                if (TX == 5) {  // timing ablation: the ids computed (escapes too), not stored
-#pragma unroll
-                    for (int j = 0; j < BLK; ++j) cnt += r[j];
-                    continue;
-                }
                 if (OUTW == 4) {
-                    // (TX = 3, timing ablation: every block's ids to the
-                    // same line per lane, which stays in L2 -- wrong ids)
-                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) +
-                                                        (TX == 3 ? (int64_t)threadIdx.x * BLK : i - pos0));
+                    uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(out) + (i - pos0));
 #pragma unroll
                     for (int q = 0; q < BLK / 4; ++q)
                         o[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
@@ -1786,16 +1573,13 @@ void dfa_sparse_lds_kernel(
 //    instruction instead of 16-B pieces of 64 lines (NT: non-temporal).
 // Every loop a lane's exchange depends on is wave-uniform (lanes without a
 // segment or past their last block take part and store nothing).
-// ABL (timing ablations, wrong ids): 1 = no escape lookups, 2 = no stores,
-// 3 = neither staging writes nor stores (the steps and the count alone).
-// O16: the escapes read the u16 copy of the output table (DfaDev::sout8h;
-// half its L2 footprint: lines 5.69 -> 5.61 ms).
-template <int OUTW, int KR, int THREADS, bool NT, int BU = 8, int ABL = 0, bool O16 = false>
+// (Product for gids past u16; its timing ablations and the u16-escape-table
+// form of round 4 are in git history.)
+template <int OUTW, int KR, int THREADS, bool NT, int BU = 8>
 __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
-    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3,
-    const uint16_t* __restrict__ outt16 = nullptr) {
+    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
     constexpr int BLK = 32, SROW = 33;  // a lane's staging row: 32 ids + one pad dword
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 1];
     __shared__ uint32_t s_ids[THREADS * SROW];
@@ -1849,14 +1633,14 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
                     const uint32_t v = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb, R);
                     s = act[tt] ? v & DFA_STATE_MASK : s;
                     cnt += act[tt] && v >= (1u << 20);  // a nonzero id (an escape is one)
-                    if (OUTW && ABL != 3) {
+                    if (OUTW) {
                         const bool esc = v >= (DFA_ESC << 20);
                         my[j] = esc ? v : v >> 20;
                         em |= esc ? 1u << j : 0u;
                     }
                 }
-                if (!OUTW || ABL == 3) return;
-                if (!act[tt] || ABL == 1) em = 0;
+                if (!OUTW) return;
+                if (!act[tt]) em = 0;
                 // (measured and removed: up to 4 / 8 escapes per lane per
                 // round, their loads issued together -- no faster, lines 5.75
                 // -> 5.74 / 5.75 ms; profiles/r04/gid_order)
@@ -1864,13 +1648,11 @@ __global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
                     if (em) {
                         const uint32_t j = __builtin_ctz(em);
                         em &= em - 1;
-                        my[j] = O16 ? (uint32_t)outt16[my[j] & DFA_STATE_MASK] : outt[my[j] & DFA_STATE_MASK];
+                        my[j] = outt[my[j] & DFA_STATE_MASK];
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
-                if (ABL == 2) {
-                    cnt += my[lane & 31];  // the staged ids read back, not stored
-                } else if (OUTW == 4) {
+                if (OUTW == 4) {
                     const uint64_t am = __ballot(act[tt]);
                     uint32_t* o = reinterpret_cast<uint32_t*>(out) + (sg0 - lane + (lane >> 3)) * seg_len + BLK * b +
                                   4 * (lane & 7);
@@ -2016,6 +1798,212 @@ __global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
             const uint32_t v = outt[s];
             out[i - pos0] = v;
             cnt += v != 0u;
+        }
+    }
+    if (count) {
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
+    }
+}
+
+// ---- the fallback-linked (FL) form (pm_flatten.h, pm_pack_sparse_fl) -----
+// The wave model of the 8-B form (scripts/sdfa_spec_model.cpp, lines stream,
+// 64 lanes in lock step) puts its wave steps at 1.77 dependent load
+// latencies: 2.3% of lane steps enter a record in a block the lane does not
+// hold and then miss its slots (the fallback row's word waits for the
+// block), and with 64 lanes 77% of wave steps hold such a lane.  In the FL
+// form the word that leads into a record names its fallback row, so a lane
+// entering a miss-prone record (not a chain interior: the word's spec bit)
+// loads the block and the fallback row's word together -- 1.22 latencies
+// per wave step modelled -- and a record carries its own output, so only
+// row outputs past the inline code escape.
+//
+// One step from the word w that led to the lane's state (state w & MASK;
+// for a record, the fallback row in bits 20-30 and the spec bit 31) on byte
+// c: returns the next word.  For a record state, own = its out16: the
+// output of the position that produced w.
+// (Ablation builds, scripts/build_ab.sh with AB_HIPFLAGS=-DPM_FL_SPEC=n:
+// 0 = never load the fallback row's word early, 2 = at every new block a
+// record with a fallback in the word enters; 1, the product: only for
+// records not in a chain interior.)
+#ifndef PM_FL_SPEC
+#define PM_FL_SPEC 1
+#endif
+template <int KR>
+__device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, uint32_t F,
+                                            const uint32_t* __restrict__ s_rows, uint32_t w, uint32_t c,
+                                            uint32_t& cb, tu32x4& R0, tu32x4& R1, uint32_t& own) {
+    const uint32_t s = w & DFA_STATE_MASK;
+    const bool isrow = s < F;
+    const uint32_t g = s - F, blk = g >> 2, e = g & 3u;
+    const uint32_t fb = (w >> 20) & PM_FL_INREC;
+    uint32_t rw = 0, fw = 0;
+    bool pre = false;
+    if (isrow) {
+        if (KR && s < (uint32_t)KR) rw = s_rows[s * 256u + c];
+        else rw = *reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
+    } else if (blk != cb) {
+        const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * 32u);
+        R0 = p[0];
+        R1 = p[1];
+        cb = blk;
+        // a miss-prone record entered in a new block: its fallback row's
+        // word in the same round of loads (LDS rows need no head start)
+        pre = (PM_FL_SPEC == 2 || (PM_FL_SPEC == 1 && (w >> 31))) && fb != PM_FL_INREC && fb >= (uint32_t)KR;
+        if (pre) fw = *reinterpret_cast<const uint32_t*>(base + fb * 1024u + c * 4u);
+    }
+    if (isrow) return rw;
+    // words 2e .. 2e + 3 of the block (a 16-B record never sits at e = 3)
+    const uint32_t w0 = (e & 2u) ? ((e & 1u) ? R1.z : R1.x) : ((e & 1u) ? R0.z : R0.x);
+    const uint32_t w1 = (e & 2u) ? ((e & 1u) ? R1.w : R1.y) : ((e & 1u) ? R0.w : R0.y);
+    own = w0 & 0xFFFFu;
+    if (c == ((w0 >> 16) & 0xFFu)) return w1;
+    const uint32_t w2 = (e & 2u) ? R1.z : ((e & 1u) ? R1.x : R0.z);
+    if (c == (w0 >> 24)) return w2;
+    if (pre) return fw;
+    const uint32_t w3 = (e & 2u) ? R1.w : ((e & 1u) ? R1.y : R0.w);
+    const uint32_t row = fb == PM_FL_INREC ? w3 : fb;
+    if (KR && row < (uint32_t)KR) return s_rows[row * 256u + c];
+    return *reinterpret_cast<const uint32_t*>(base + row * 1024u + c * 4u);
+}
+
+// The output of the position that produced w: a record's own out16 (its
+// block loaded into R0 / R1 if the lane does not hold it -- the next step's
+// load, made early), or a row word's code; *esc = the code escapes (the
+// answer is then rowout16[w & MASK]).
+__device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, uint32_t F, uint32_t w, uint32_t& cb,
+                                              tu32x4& R0, tu32x4& R1, bool& esc) {
+    const uint32_t s = w & DFA_STATE_MASK;
+    esc = false;
+    if (s < F) {
+        esc = (w >> 20) == DFA_ESC;
+        return w >> 20;
+    }
+    const uint32_t g = s - F, blk = g >> 2, e = g & 3u;
+    if (blk != cb) {
+        const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * 32u);
+        R0 = p[0];
+        R1 = p[1];
+        cb = blk;
+    }
+    const uint32_t w0 = (e & 2u) ? ((e & 1u) ? R1.z : R1.x) : ((e & 1u) ? R0.z : R0.x);
+    return w0 & 0xFFFFu;
+}
+
+// The FL form's scan: the staged-id structure of dfa_sparse_stage16_kernel
+// (u16 staging rows, escapes in rounds, whole-line non-temporal stores;
+// 1,024-lane workgroups, KR rows in LDS -- here the KR rows records fall
+// back to most), the FL step, and outputs one step late: a step writes the
+// output of the position before it (the state it starts from holds it).
+template <int KR, bool NT = true>
+__global__ __launch_bounds__(1024) void dfa_fl_kernel(
+    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* __restrict__ out,
+    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
+    const uint16_t* __restrict__ rowout16, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
+    constexpr int THREADS = 1024, BLK = 32, SROW = 17;
+    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
+    __shared__ uint32_t s_ids[THREADS * SROW];
+    {
+        const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_rows);
+        for (uint32_t k = threadIdx.x; k < nr * 64u; k += THREADS) dst[k] = src[k];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    uint16_t* const my = reinterpret_cast<uint16_t*>(s_ids + threadIdx.x * SROW);
+    const uint32_t* const wrows = s_ids + (threadIdx.x - lane) * SROW;  // the wave's rows
+    const int64_t nseg = (n + seg_len - 1) / seg_len;
+    const int64_t lanes = (int64_t)gridDim.x * THREADS;
+    uint32_t cnt = 0, cb = 0xFFFFFFFFu, own = 0;
+    tu32x4 R0 = {0u, 0u, 0u, 0u}, R1 = {0u, 0u, 0u, 0u};
+    for (int64_t sg0 = (int64_t)blockIdx.x * THREADS + threadIdx.x; __ballot(sg0 < nseg); sg0 += lanes) {
+        const bool has = sg0 < nseg;
+        const int64_t lo = has ? pos0 + sg0 * seg_len : pos0 + n;
+        const int64_t hi = has ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : pos0 + n;
+        int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
+        if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
+        uint32_t w = 0;  // the root, reached by no word
+        for (int64_t i = wlo; i < lo; ++i) w = fl_step<KR>(base, F, s_rows, w, text[i], cb, R0, R1, own);
+        const int64_t nblk = seg_len / BLK;
+        for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
+            bool act[2];
+            uint32_t WT[2][8];
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) {
+                act[tt] = lo + BLK * (b0 + tt) + BLK <= hi;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const tu32x4* tp = reinterpret_cast<const tu32x4*>(text + lo + BLK * (b0 + tt) + 16 * q);
+                    const tu32x4 v = act[tt] ? *tp : tu32x4{0u, 0u, 0u, 0u};
+                    WT[tt][4 * q] = v.x;
+                    WT[tt][4 * q + 1] = v.y;
+                    WT[tt][4 * q + 2] = v.z;
+                    WT[tt][4 * q + 3] = v.w;
+                }
+            }
+            if (!__ballot(act[0])) break;
+            unroll_for<0, 2>([&](auto tc) {
+                constexpr int tt = decltype(tc)::value;
+                if (tt == 1 && !__ballot(act[1])) return;
+                const int64_t b = b0 + tt;
+                uint32_t em = 0;
+#pragma unroll
+                for (int j = 0; j < BLK; ++j) {
+                    const uint32_t wn = fl_step<KR>(base, F, s_rows, w, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb,
+                                                    R0, R1, own);
+                    if (j > 0) {  // the output of position j - 1, which produced w
+                        const bool rec = (w & DFA_STATE_MASK) >= F;
+                        const uint32_t code = w >> 20;
+                        const bool esc = !rec && code == DFA_ESC;
+                        const uint32_t id = rec ? own : code;
+                        my[j - 1] = (uint16_t)(esc ? (w & DFA_STATE_MASK) : id);
+                        em |= esc ? 1u << (j - 1) : 0u;
+                        cnt += act[tt] && id != 0u;  // an escape is a nonzero id
+                    }
+                    w = act[tt] ? wn : w;
+                }
+                {  // position 31
+                    bool esc;
+                    const uint32_t id = fl_output(base, F, w, cb, R0, R1, esc);
+                    my[BLK - 1] = (uint16_t)(esc ? (w & DFA_STATE_MASK) : id);
+                    em |= esc ? 1u << (BLK - 1) : 0u;
+                    cnt += act[tt] && id != 0u;
+                }
+                if (!act[tt]) em = 0;
+                while (__ballot(em != 0)) {  // row outputs past the inline code: one per lane per round
+                    if (em) {
+                        const uint32_t j = __builtin_ctz(em);
+                        em &= em - 1;
+                        my[j] = rowout16[my[j]];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                const uint64_t am = __ballot(act[tt]);
+                uint32_t* o = out + (sg0 - lane + (lane >> 3)) * seg_len + BLK * b + 4 * (lane & 7);
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int cc = 8 * t + (lane >> 3);
+                    const uint32_t* src = wrows + cc * SROW + 2 * (lane & 7);
+                    const uint32_t w0 = src[0], w1 = src[1];
+                    const tu32x4 v = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
+                    if ((am >> cc) & 1u) {
+                        if (NT) __builtin_nontemporal_store(v, reinterpret_cast<tu32x4*>(o));
+                        else *reinterpret_cast<tu32x4*>(o) = v;
+                    }
+                    o += 8 * seg_len;
+                }
+                __builtin_amdgcn_wave_barrier();
+            });
+        }
+        // the segment's last (< BLK) positions
+        for (int64_t i = lo + BLK * ((hi - lo) / BLK); i < hi; ++i) {
+            w = fl_step<KR>(base, F, s_rows, w, text[i], cb, R0, R1, own);
+            bool esc;
+            uint32_t id = fl_output(base, F, w, cb, R0, R1, esc);
+            if (esc) id = rowout16[w & DFA_STATE_MASK];
+            out[i - pos0] = id;
+            cnt += id != 0u;
         }
     }
     if (count) {
@@ -2172,20 +2160,8 @@ __global__ void gen_stream_kernel(uint8_t* __restrict__ dst, uint64_t off, uint6
 //   4 MiB: 32 / 64 / 128 / 256 workgroups 0.036 / 0.027 / 0.035 / 0.059
 //   16 MiB:                              0.101 / 0.058 / 0.049 / 0.067
 //   64 MiB:                              0.366 / 0.193 / 0.116 / 0.104
-static int g_rt_max_blocks = 0;  // pm_rt_set_max_blocks (timing sweeps); 0 = the rule above
-// Launches of at most this many positions take rt_small_kernel
-// (pm_rt_set_small_max; 0 = never).
-static int64_t g_rt_small_max = (int64_t)256 << 10;
-// ... staging each workgroup's text window in LDS first (pm_rt_set_small_stage;
-// off: no faster at read_block's 100 KiB zero-copy calls, 40.6 against 39.3
-// us per call, profiles/r04/host_path/small_call_variants_ab.json)
-static bool g_rt_small_stage = false;
 static int64_t rt_blocks(int64_t n, int num_cu) {
     const int64_t nchunks = (n + RT_CHUNK - 1) / RT_CHUNK;
-    if (g_rt_max_blocks > 0) {
-        const int64_t b = (nchunks + RT_WAVES - 1) / RT_WAVES, cap = g_rt_max_blocks < num_cu ? g_rt_max_blocks : num_cu;
-        return b > cap ? cap : (b < 1 ? 1 : b);
-    }
     const int64_t one_each = (nchunks + RT_WAVES - 1) / RT_WAVES;     // one chunk per wave
     const int64_t eight_each = (nchunks + 8 * RT_WAVES - 1) / (8 * RT_WAVES);
     const int64_t floor_b = one_each < num_cu / 4 ? one_each : num_cu / 4;
@@ -2193,9 +2169,9 @@ static int64_t rt_blocks(int64_t n, int num_cu) {
     if (b > num_cu) b = num_cu;
     return b < 1 ? 1 : b;
 }
-void pm_rt_set_max_blocks(int b) { g_rt_max_blocks = b > 0 ? b : 0; }
-void pm_rt_set_small_max(int64_t n) { g_rt_small_max = n >= 0 ? n : ((int64_t)256 << 10); }
-void pm_rt_set_small_stage(int on) { g_rt_small_stage = on != 0; }
+// Launches of at most this many positions take rt_small_kernel (RtDev::
+// small_max overrides it per object: 0 = never).
+constexpr int64_t RT_SMALL_MAX = (int64_t)256 << 10;
 // Spill items per wave region: one per position of the wave's main-loop
 // chunks, capped at RT_SPILL_WAVE_CAP (the kernel resolves a full region
 // and goes on, rt_scan_kernel): 128 KiB per wave, 512 MiB for a 1 GiB launch
@@ -2203,26 +2179,26 @@ void pm_rt_set_small_stage(int on) { g_rt_small_stage = on != 0; }
 // deep streams (1 GiB snort, dense / count, profiles/r03/spill_cap_ab.txt)
 // caps of 16 / 32 / 64 / 128 chunks and the unbounded region measured
 // equal (shipped 11.33-11.37 ms, lines 15.68-15.86 ms; random ASCII equal).
-#ifndef RT_SPILL_CAP_CHUNKS
-#define RT_SPILL_CAP_CHUNKS 16
-#endif
-constexpr int64_t RT_SPILL_WAVE_CAP = RT_SPILL_CAP_CHUNKS * RT_CHUNK;
-static int64_t g_spill_cap = RT_SPILL_WAVE_CAP;  // pm_rt_set_spill_cap (tests: >= one chunk)
-static int64_t rt_spill_stride(int64_t n, int64_t blocks) {
+// RtDev::spill_cap_chunks lowers it per object (tests: small launches then
+// resolve full regions many times).
+constexpr int64_t RT_SPILL_CAP_CHUNKS = 16;
+static int64_t rt_wave_cap(int64_t cap_chunks) {
+    return (cap_chunks >= 1 && cap_chunks < RT_SPILL_CAP_CHUNKS ? cap_chunks : RT_SPILL_CAP_CHUNKS) * RT_CHUNK;
+}
+static int64_t rt_spill_stride(int64_t n, int64_t blocks, int64_t wave_cap) {
     const int64_t nw = blocks * RT_WAVES;
     const int64_t natural = ((n / RT_CHUNK + nw - 1) / nw) * RT_CHUNK;
-    return natural < g_spill_cap ? natural : g_spill_cap;
+    return natural < wave_cap ? natural : wave_cap;
 }
-void pm_rt_set_spill_cap(int chunks) { g_spill_cap = chunks >= 1 ? (int64_t)chunks * RT_CHUNK : RT_SPILL_WAVE_CAP; }
 
-int64_t pm_rt_spill_items(int64_t n, int num_cu) {
+int64_t pm_rt_spill_items(int64_t n, int num_cu, int64_t cap_chunks) {
     constexpr int64_t PIECE = (int64_t)RT_POSMASK + 1;
     const int64_t m = n > PIECE ? PIECE : n;
     const int64_t blocks = rt_blocks(m, num_cu);
-    return blocks * RT_WAVES * rt_spill_stride(m, blocks);
+    return blocks * RT_WAVES * rt_spill_stride(m, blocks, rt_wave_cap(cap_chunks));
 }
 
-static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
+static hipError_t launch_rt_impl(bool floor, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
                                  void* out, int outw, unsigned long long* count, const RtDev& t0, int num_cu,
                                  hipStream_t s) {
     if (n <= 0) return hipSuccess;
@@ -2234,475 +2210,194 @@ static hipError_t launch_rt_impl(int variant, const uint8_t* text, int64_t strea
         for (int64_t off = 0; off < n; off += PIECE) {
             const int64_t m = n - off < PIECE ? n - off : PIECE;
             void* o = outw ? reinterpret_cast<uint8_t*>(out) + off * outw : nullptr;
-            hipError_t e = launch_rt_impl(variant, text, stream_start, pos0 + off, m, o, outw, count, t0, num_cu, s);
+            hipError_t e = launch_rt_impl(floor, text, stream_start, pos0 + off, m, o, outw, count, t0, num_cu, s);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    if (variant == 0 && n <= g_rt_small_max) {  // small launch: one thread per position
+    const int64_t small_max = t0.small_max >= 0 ? t0.small_max : RT_SMALL_MAX;
+    if (!floor && n <= small_max) {  // small launch: one thread per position
         const dim3 gs((unsigned)((n + RT_SMALL_THREADS - 1) / RT_SMALL_THREADS)), bs(RT_SMALL_THREADS);
-        const bool stage = g_rt_small_stage && t0.back <= (uint32_t)RT_SMALL_BACK_MAX &&
-                           ((uintptr_t)text & 3) == 0;
-#define PM_RT_SMALL(W, ST) \
-    hipLaunchKernelGGL((rt_small_kernel<W, ST>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0)
-        if (stage) {
-            if (outw == 4) PM_RT_SMALL(4, true);
-            else if (outw == 2) PM_RT_SMALL(2, true);
-            else PM_RT_SMALL(0, true);
-        } else {
-            if (outw == 4) PM_RT_SMALL(4, false);
-            else if (outw == 2) PM_RT_SMALL(2, false);
-            else PM_RT_SMALL(0, false);
-        }
-#undef PM_RT_SMALL
+        if (outw == 4) hipLaunchKernelGGL((rt_small_kernel<4>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
+        else if (outw == 2) hipLaunchKernelGGL((rt_small_kernel<2>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
+        else hipLaunchKernelGGL((rt_small_kernel<0>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, t0);
         return hipGetLastError();
     }
     const int64_t blocks = rt_blocks(n, num_cu);
     RtDev t = t0;
-    t.spill_stride = rt_spill_stride(n, blocks);
-    // The caller sizes the scratch (pm_rt_spill_items) with the cap in force
-    // then; a cap raised since (pm_rt_set_spill_cap, timing sweeps) must not
-    // turn a scratch sized before it into a failed launch: the stride is
-    // clamped to what the scratch holds, whole chunks, at least one (the
-    // kernel resolves a full region and goes on, so any stride of >= one
-    // chunk is exact).
+    t.spill_stride = rt_spill_stride(n, blocks, rt_wave_cap(t0.spill_cap_chunks));
+    // The caller sizes the scratch (pm_rt_spill_items); a launch whose
+    // scratch holds less than the stride clamps it to whole chunks, at least
+    // one (the kernel resolves a full region and goes on, so any stride of
+    // >= one chunk is exact).
     const int64_t fit = t.spill_cap / (blocks * RT_WAVES) / RT_CHUNK * RT_CHUNK;
     if (t.spill_stride > fit) {
         if (fit < RT_CHUNK) return hipErrorInvalidValue;  // scratch smaller than one chunk per wave
         t.spill_stride = fit;
     }
     const dim3 g((unsigned)blocks), b(RT_THREADS);
-#define RT_LAUNCH(VV)                                                                                             \
-    do {                                                                                                          \
-        if (outw == 4)                                                                                            \
-            hipLaunchKernelGGL((rt_scan_kernel<VV, 4>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
-        else if (outw == 2)                                                                                       \
-            hipLaunchKernelGGL((rt_scan_kernel<VV, 2>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
-        else                                                                                                      \
-            hipLaunchKernelGGL((rt_scan_kernel<VV, 0>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
-    } while (0)
-#define RT_LAUNCH_EF(VV)                                                                                          \
-    do {                                                                                                          \
-        if (outw == 4)                                                                                            \
-            hipLaunchKernelGGL((rt_scan_kernel<VV, 4, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
-        else if (outw == 2)                                                                                       \
-            hipLaunchKernelGGL((rt_scan_kernel<VV, 2, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
-        else                                                                                                      \
-            hipLaunchKernelGGL((rt_scan_kernel<VV, 0, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t); \
-    } while (0)
-    switch (variant) {
-        case 100: RT_LAUNCH_EF(0); break;  // early prefetch (timing experiment)
-        case 102: RT_LAUNCH_EF(2); break;
-        case 1: RT_LAUNCH(1); break;
-        case 2: RT_LAUNCH(2); break;
-        case 3: RT_LAUNCH(3); break;
-        case 4: RT_LAUNCH(4); break;
-        case 5: RT_LAUNCH(5); break;
-        case 6: RT_LAUNCH(6); break;
-        case 7: RT_LAUNCH(7); break;
-        case 8: RT_LAUNCH(8); break;
-        case 9: RT_LAUNCH(9); break;
-        case 10: RT_LAUNCH(10); break;
-        case 12: RT_LAUNCH(12); break;
-        case 13: RT_LAUNCH_EF(13); break;
-        case 14: RT_LAUNCH_EF(14); break;
-        case 15: RT_LAUNCH_EF(15); break;
-        default:
-            // early prefetch for u16 ids and count only (0.864 -> 0.847 ms,
-            // 0.565 -> 0.547); u32 ids would spill (1.166 -> 1.216)
-            if (outw == 4) RT_LAUNCH(0);
-            else RT_LAUNCH_EF(0);
+    // early prefetch (EF) for u16 ids and count only (0.864 -> 0.847 ms,
+    // 0.565 -> 0.547); u32 ids would spill (1.166 -> 1.216)
+    if (floor) {
+        if (outw == 4) hipLaunchKernelGGL((rt_scan_kernel<2, 4>), g, b, 0, s, text, stream_start, pos0, n, out, count, t);
+        else if (outw == 2) hipLaunchKernelGGL((rt_scan_kernel<2, 2>), g, b, 0, s, text, stream_start, pos0, n, out, count, t);
+        else hipLaunchKernelGGL((rt_scan_kernel<2, 0>), g, b, 0, s, text, stream_start, pos0, n, out, count, t);
+    } else if (outw == 4) {
+        hipLaunchKernelGGL((rt_scan_kernel<0, 4>), g, b, 0, s, text, stream_start, pos0, n, out, count, t);
+    } else if (outw == 2) {
+        hipLaunchKernelGGL((rt_scan_kernel<0, 2, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t);
+    } else {
+        hipLaunchKernelGGL((rt_scan_kernel<0, 0, true>), g, b, 0, s, text, stream_start, pos0, n, out, count, t);
     }
-#undef RT_LAUNCH
-#undef RT_LAUNCH_EF
     return hipGetLastError();
 }
 
 hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                         unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s) {
-    return launch_rt_impl(0, text, stream_start, pos0, n, out, outw, count, t, num_cu, s);
+    return launch_rt_impl(false, text, stream_start, pos0, n, out, outw, count, t, num_cu, s);
 }
 
-hipError_t pm_launch_rt_variant(int variant, const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n,
-                                void* out, int outw, unsigned long long* count, const RtDev& t, int num_cu,
-                                hipStream_t s) {
-    return launch_rt_impl(variant, text, stream_start, pos0, n, out, outw, count, t, num_cu, s);
+hipError_t pm_launch_rt_floor(const uint8_t* text, int64_t n, void* out, int outw, const RtDev& t, int num_cu,
+                              hipStream_t s) {
+    return launch_rt_impl(true, text, 0, 0, n, out, outw, nullptr, t, num_cu, s);
 }
 
-// DFA launch shape: lanes (segments in flight) per CU; pm_dfa_set_shape
-// sweeps it.  More lanes than this measured slower: the gathers then touch
-// more distinct table lines than the caches hold.
-constexpr int DFA_LANES_PER_CU = 512;
-static int g_dfa_lanes_per_cu = DFA_LANES_PER_CU;
-static bool g_dfa_shape_forced = false;  // pm_dfa_set_shape: every form at the swept lanes
-// Shortest segment.  A launch of fewer segments than lanes is latency-bound
-// (each lane's chain of max_len-1 warm-up + segment dependent steps is the
-// launch time), so short launches want short segments, at the price of
-// more warm-up steps: n / 65536 clamped to [64, 512] bytes.  Measured
-// (scripts/dfa_seg_sweep.py, profiles/r02/dfa_segment_sweep.txt), against
-// the round-1 fixed 2 KiB: 100 KiB 0.34 -> 0.07 ms, 1 MiB 0.62 -> 0.07,
-// 16 MiB 0.76-0.86 -> 0.28-0.37, 64 MiB 1.06-1.43 -> 0.59-0.73; from 256
-// MiB up the lane cap decides and nothing changes.
-static int64_t g_dfa_min_seg = 0;  // pm_dfa_set_min_seg override (timing sweeps)
-// segments per lane of the output-coded kernel (profiles/r02/dfa_coded_ab.txt:
-// two chains at 512 lanes per CU beat the uncoded kernel on random ASCII,
-// the tiled shipped stream and the lines stream; one chain lost on the
-// shipped stream)
-// The sparse form (its step has a second, dependent load at a record miss)
-// measured best at one chain: lines stream 10.2 ms at 512 lanes x 1 against
-// 15.4 at x 2 (scripts/dfa_coded_sweep.py).
-constexpr int DFA_CHAINS = 2, SDFA_CHAINS = 1;
-// Positions per block of the sparse kernel at one chain (16 or 32;
-// pm_dfa_set_block): 32 stores one whole 128-B line of u32 ids per lane and
-// measured 6-15% faster on every stream (lines 10.23 -> 9.63 ms, shipped
-// 10.8 -> 9.7, ASCII 6.82 -> 6.15 at 512 lanes per CU; profiles/r02).
-constexpr int SDFA_BLK = 32;
-static int g_sdfa_blk = SDFA_BLK;
-// The dense coded kernel: 32 positions per block (one whole 128-B line of
-// u32 ids per lane and segment) measured faster at every shape: shipped
-// stream 4.32 -> 3.84 ms, ASCII 6.58 -> 5.93, lines 20.5 -> 19.8 at 512
-// lanes x 2 segments (profiles/r02/dfa_dense_block_sweep.txt); with u16 ids
-// 5.23 -> 4.30, 6.40 -> 5.58, 19.8 -> 19.3 (dfa_dense_u16_block_ab.txt).
-constexpr int DFA_DENSE_BLK = 32;
-static int g_dfa_dense_blk = DFA_DENSE_BLK;
-static int g_sdfa_var = 0;  // timing experiments (dfa_sparse_kernel VAR; 8 = 64-position blocks)
-// The sparse form's kernel: 0 = dfa_sparse_kernel, 1 = dfa_sparse_lds_kernel
-// (LDS rows + register record blocks), 2 = the latter without LDS rows,
-// 3 / 4 = (1) with two segments per lane (16 / 32-position blocks), 5 / 6 =
-// (2) with two segments per lane, 7 = (2) with 16-position blocks, 8 = (7)
-// with registers capped for 6 waves per SIMD, 9 = (2) over the 8-B record
-// units of pm_pack_sparse8 (2 when the automaton has none), 10 = (9) with
-// the text of two blocks per load, 11 / 12 = (10) with the first 32 / 64
-// rows in LDS, 22-24 = timing ablations of (12)'s id output, 25-28 =
-// dfa_sparse_stage_kernel (ids staged in LDS, escapes in rounds, whole-line
-// stores; 27: 1024-lane workgroups with 16 LDS rows, 28: 27 with 4-unit
-// record blocks; 34: 28 with the u16 escape table; 35 / 36: u16 staging
-// rows with 88 / 48 LDS rows); -1 = the product choice: 35 (28 without a
-// u16 table) for u32 ids, 12 for u16, 10
-// for count only, at SDFA_LANES_PER_CU.  Round 4, side by side (snort,
-// 1 GiB, dense u32, ms; profiles/r04/dyn): lines / shipped / ASCII
-//   12  6.50 / 4.60 / 5.19    27  6.17 / 4.40 / 5.00    28  6.19 / 4.10 / 4.11
-// and 28 with gids numbered by output frequency (pm_assign_gids: 5.1% of
-// the lines stream's outputs escape instead of 13.7%): 5.75 / 3.86 / 4.10;
-// 34 = 28 with the u16 escape table: 5.61 / 3.80 / 4.10 against 5.69 /
-// 3.80 / 4.07 side by side; 35 / 36 = dfa_sparse_stage16_kernel (u16
-// staging rows, 88 / 48 LDS rows; the product for u32 ids when every gid
-// fits is 35): 5.58 / 3.75 / 3.77 and 5.64 / 3.87 / 4.00 against 34's
-// 5.63 / 3.85 / 4.08 (profiles/r04/gid_order/stage16_ab.json).
-// (u16 ids: 27 and 28 are 3-8% slower than 12, which keeps them).  Side by side at 512 lanes per CU (snort, 1 GiB,
-// ms; profiles/r03/sdfa_lds_ab.json, PMC in sdfa_lds_pmc.json; the 3 / 4
-// rows are the round's first two-segment build, whose register arrays the
-// compiler had put in scratch):
-//            lines dense / count   shipped dense / count   ASCII dense / count
-//   0         9.64 / 8.05          10.04 / 5.82            6.25 / 4.85
-//   1         9.82 / 8.77           8.69 / 6.05            6.09 / 5.06
-//   2         9.43 / 8.24           8.78 / 5.90            7.06 / 5.83
-//   3 / 4    29.4 / 26.2 ...       18.3 / 16.7 ...         19.8 / 17.4 ...
-// The PMC says why the LDS rows and the record blocks move the lines stream
-// so little: they cut the L2 requests by 45% (TCP_TCC_READ_REQ 1.30 G ->
-// 0.72 G per launch, all of them L2 hits), but the L2 misses -- the table
-// lines that come from the Infinity Cache or HBM, 0.39 G per launch either
-// way -- are what the kernel waits for; two segments per lane double them.
-// What does move it is the number of chains a CU keeps in flight: (2) holds
-// a position's coded word in one register (118 VGPRs: 4 waves per SIMD), so
-// two 512-lane workgroups fit a CU.  Lanes per CU (profiles/r03/
-// sdfa_lanes_*.txt, sdfa_occupancy_sweep.txt; dense u32 / count only, ms):
-//                 lines          shipped        ASCII
-//   (2) x 512     9.43 / 8.28    8.57 / 5.83    7.13 / --
-//   (2) x 1024    8.89 / 6.73    5.77 / 4.74    7.19 / 5.95
-//   (2) x 1536    10.19 / 8.39   7.37 / 6.26    7.86 / 6.76   (6 WGs on 4 slots)
-//   (8) x 1536    11.53 / 9.03   8.14 / 6.63    8.87 / 7.25   (3 resident WGs)
-//   (0) x 512     9.17 / 8.02    8.74 / 5.61
-// Past two workgroups per CU every stream slows down, resident or not:
-// the table gathers then saturate the memory system.  Two segments per
-// lane at 512 lanes (5 / 6, no scratch now) measured 10.3 / 10.75 ms on
-// the lines stream.  8-B record units (9; 75% of snort's records are one
-// unit, so a 128-B line holds twice the states of a pattern's run) against
-// (2) at 1024 lanes, side by side (profiles/r03/sdfa_units8_ab.txt; dense /
-// u16 / count, ms): lines 9.04 / 8.58 / 6.83 -> 8.42 / 7.93 / 6.73, shipped
-// 5.83 / 5.32 / 4.75 -> 5.85 / 5.47 / 4.80, ASCII 7.22 / 6.87 / 5.96 ->
-// 7.20 / 6.89 / 6.01.  Two blocks' text per load (10 against 9; 128 VGPRs,
-// still 4 waves; profiles/r03/sdfa_text_two_blocks_ab.txt): lines 8.36 /
-// 7.93 / 6.71 -> 8.16 / 7.72 / 6.49, shipped 5.88 / 5.48 / 4.73 -> 5.76 /
-// 5.33 / 4.63, ASCII dense 7.20 -> 6.97.  The root and the 63 shallowest
-// rows staged in LDS (12, 64 KiB per workgroup, two still fit a CU) against
-// (10), side by side (profiles/r03/sdfa_lds_rows_units8_ab.txt; dense / u16
-// / count): lines 8.20 / 7.74 / 6.42 -> 8.12 / 7.70 / 6.61, shipped 5.75 /
-// 5.33 / 4.63 -> 5.69 / 5.21 / 4.51, ASCII 6.98 / -- / 5.67 -> 6.60 / -- /
-// 5.41; 32 rows (11) measured equal to (10).  Ids take the tile, count only
-// (whose lines stream it slows) does not.  Measured and removed (profiles/r03/
-// sdfa_pipelined_ids_ab.txt, lines / shipped / ASCII, dense u32): (2) with
-// non-temporal id stores 11.9 / 8.9 / 8.9 ms against 9.0 / 5.8 / 7.2; the
-// ids of block b resolved and stored one 16-B chunk per step of block b + 1
-// (so the escape lookups and the stores would overlap the next table loads
-// instead of stalling a block's end) 13.1 / 8.5 / 9.7: a store interleaved
-// with the steps puts its L2 acknowledgement on the chain (vmcnt retires in
-// order) at steps whose table load is a register or L2 hit, eight times a
-// block instead of once.
-constexpr int SDFA_LANES_PER_CU = 1024;
-constexpr int DFA_COUNT_LANES_PER_CU = 1024;
-static int g_sdfa_lds = -1;
-// Warm-ups start at the last synchronizing 3-gram (dfa_sync_lo; the sparse
-// forms 10-12 and the dense coded kernel; 0: always max_len - 1 bytes back,
-// timing).  Side by side, 1 GiB snort, ms with 0 -> 1 (profiles/r03/
-// dfa_sync_ab.txt): sparse ids lines 8.15 -> 6.61, shipped 5.76 -> 4.63,
-// ASCII 6.62 -> 5.21; sparse count only 6.51 -> 4.92 / 4.61 -> 3.43 /
-// 5.67 -> 4.29; dense ids 19.70 -> 17.32 / 4.02 -> 3.53 / 5.96 -> 4.78.
-constexpr int kDfaSyncDefault = 1;
-static int g_dfa_sync = kDfaSyncDefault;
-static int g_dfa_chains = 0;  // 0: the form's default
-// dense rows or the sparse form for output-coded automata, when a launch
-// does not name one (-1: not forced; the plugin then times both forms)
-static int g_dfa_sparse = -1;
+// ---- DFA launches ----------------------------------------------------------
+// Dense rows (dfa_coded_kernel): 512 lanes per CU, two chains per lane in
+// lock step (two gathers in flight), 32-position blocks with ids (one whole
+// 128-B line of u32 ids per lane and chain: shipped stream 4.32 -> 3.84 ms,
+// ASCII 6.58 -> 5.93, lines 20.5 -> 19.8; u16 5.23 -> 4.30 / 6.40 -> 5.58 /
+// 19.8 -> 19.3; profiles/r02/dfa_dense_block_sweep.txt), 1,024 lanes per CU
+// for count only once warm-ups start at a synchronizing 3-gram (shipped
+// 3.28 -> 2.47 ms, ASCII 4.04 -> 4.10; profiles/r03/dfa_sync_lanes.txt).
+// More lanes measured slower: the gathers then touch more distinct table
+// lines than the caches hold.  The uncoded kernel (automata of 2^20 states
+// or more): one chain per lane.
+constexpr int DFA_LANES_PER_CU = 512, DFA_COUNT_LANES_PER_CU = 1024, DFA_CHAINS = 2, DFA_DENSE_BLK = 32;
+// The sparse form: 1,024 lanes per CU (two 512-lane lock-step workgroups,
+// or one 1,024-lane staged workgroup), one chain per lane, 32-position
+// blocks (profiles/r03/sdfa_lanes_*.txt, sdfa_occupancy_sweep.txt:
+// past 1,024 lanes per CU every stream slows down).
+constexpr int SDFA_LANES_PER_CU = 1024, SDFA_BLK = 32;
+// Shortest segment: a launch of fewer segments than lanes is latency-bound
+// (each lane's chain of warm-up + segment steps is the launch time), so
+// short launches take short segments, n / 65536 clamped to [64, 512] bytes
+// (against the round-1 fixed 2 KiB: 100 KiB 0.34 -> 0.07 ms, 1 MiB 0.62 ->
+// 0.07, 16 MiB 0.76-0.86 -> 0.28-0.37, 64 MiB 1.06-1.43 -> 0.59-0.73;
+// scripts/dfa_seg_sweep.py, profiles/r02/dfa_segment_sweep.txt).
+//
+// Product kernels of the sparse form, by output width (DfaDev::sparse_kernel
+// 0; side by side histories in DESIGN.md §4):
+//   u32 ids    the fallback-linked form (dfa_fl_kernel, PM_SK_FL); without
+//              it (>= 65,536 rows) the u16-staged 8-B-unit kernel
+//              (dfa_sparse_stage16_kernel<88, 4>, PM_SK_STAGE16); with gids
+//              past u16 the u32-staged one (dfa_sparse_stage_kernel,
+//              PM_SK_STAGE); without 8-B units (ids past 2^20) the lock-step
+//              kernel over the 16-B records (PM_SK_LOCK16)
+//   u16 ids    the lock-step kernel over 8-B units with the root and the 63
+//              shallowest rows in LDS (PM_SK_LOCK8), else PM_SK_LOCK16
+//   count      the lock-step kernel over 8-B units without LDS rows
+//              (PM_SK_LOCK8), else PM_SK_LOCK16
+// A forced kernel (DfaDev::sparse_kernel; tests, A/B timing) runs where the
+// object has its image and it writes the width asked for; other launches
+// take the product choice (pm_dfa_sparse_choice reports which ran).
+int pm_dfa_sparse_choice(const DfaDev& t, int outw) {
+    if (!(t.coded && t.sbase && t.form != 1)) return 0;
+    const int sk = t.sparse_kernel;
+    const bool ok = sk == PM_SK_FL       ? t.flbase && outw == 4
+                    : sk == PM_SK_STAGE16 ? t.sout8h && outw == 4
+                    : sk == PM_SK_STAGE   ? t.sbase8 && outw != 0
+                    : sk == PM_SK_LOCK8   ? t.sbase8 != nullptr
+                                          : sk == PM_SK_LOCK16;
+    if (ok) return sk;
+    return outw == 4 ? (t.flbase ? PM_SK_FL : t.sout8h ? PM_SK_STAGE16 : t.sbase8 ? PM_SK_STAGE : PM_SK_LOCK16)
+                     : (t.sbase8 ? PM_SK_LOCK8 : PM_SK_LOCK16);
+}
 
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                          unsigned long long* count, const DfaDev& t, int num_cu, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (!out) outw = 0;
     if (outw != 0 && outw != 2 && outw != 4) return hipErrorInvalidValue;
-    // one segment per lane and chain, none shorter than short_seg (above)
-    const bool sparse = t.coded && t.sbase && (t.form ? t.form == 2 : g_dfa_sparse != 0);
-    // (without 8-B units -- an automaton whose unit ids pass 2^20 -- the
-    // staged kernels cannot run: 12 / 10 then take the 16-B records)
-    const int sdfa_lds = g_sdfa_lds >= 0 ? g_sdfa_lds
-                         : outw == 4        ? (t.sout8h ? 35 : t.sbase8 ? 28 : 12)
-                         : outw             ? 12
-                                            : 10;
-    const bool lds2 = sparse && sdfa_lds >= 3 && sdfa_lds <= 6 && !g_sdfa_var && !g_dfa_chains;  // LDS kernel, two segments per lane
-    const int64_t ch = !t.coded ? 1 : g_dfa_chains ? g_dfa_chains : lds2 ? 2 : sparse ? SDFA_CHAINS : DFA_CHAINS;
-    const bool lds_kernel = sparse && sdfa_lds && !g_sdfa_var && !g_dfa_chains;
-    const uint32_t* g3 = g_dfa_sync ? t.gram3 : nullptr;  // synchronizing 3-grams (DfaDev::gram3)
-    // (dense rows, count only: 1,024 lanes per CU once warm-ups start at a
-    // synchronizing 3-gram -- shipped 3.28 -> 2.47 ms, ASCII 4.04 -> 4.10;
-    // profiles/r03/dfa_sync_lanes.txt)
-    const int lanes_cu = g_dfa_shape_forced ? g_dfa_lanes_per_cu
-                         : lds_kernel       ? SDFA_LANES_PER_CU
-                         : t.coded && !sparse && outw == 0 ? DFA_COUNT_LANES_PER_CU
-                                                           : DFA_LANES_PER_CU;
+    const uint32_t* g3 = t.sync ? t.gram3 : nullptr;  // warm-ups from synchronizing 3-grams
+    const int sk = pm_dfa_sparse_choice(t, outw);
+    const bool sparse = sk != 0;
+    // segments: one per lane and chain, none shorter than short_seg, whole
+    // blocks
+    const int64_t ch = !t.coded ? 1 : sparse ? 1 : DFA_CHAINS;
+    const int lanes_cu = sparse ? SDFA_LANES_PER_CU : t.coded && outw == 0 ? DFA_COUNT_LANES_PER_CU : DFA_LANES_PER_CU;
     const int64_t lanes = (int64_t)num_cu * lanes_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
-    const int64_t short_seg = g_dfa_min_seg ? g_dfa_min_seg : std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
+    const int64_t short_seg = std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
     if (seg < short_seg) seg = short_seg;
-    const int64_t align = sparse && (ch == 1 || outw == 4) ? ((g_sdfa_var & 8) ? 64 : g_sdfa_blk)
-                          : !sparse && t.coded && outw != 0 ? g_dfa_dense_blk
-                                                            : 16;  // whole blocks per segment
+    const int64_t align = sparse ? SDFA_BLK : t.coded && outw != 0 ? DFA_DENSE_BLK : 16;
     seg = (seg + align - 1) / align * align;
     const int64_t nseg = (n + seg - 1) / seg;
+    if (sparse) {
+        // persistent workgroups (LDS staged once each), at most one lane per
+        // segment and SDFA_LANES_PER_CU lanes per CU
+        const int wgt = sk == PM_SK_FL || sk == PM_SK_STAGE16 || sk == PM_SK_STAGE ? 1024 : DFA_LDS_THREADS;
+        int64_t wg = (nseg + wgt - 1) / wgt;
+        const int64_t cap = lanes / wgt;
+        if (wg > cap) wg = cap;
+        if (wg < 1) wg = 1;
+        const dim3 gs((unsigned)wg), bs(wgt);
+        switch (sk) {
+            case PM_SK_FL:
+                hipLaunchKernelGGL((dfa_fl_kernel<88, true>), gs, bs, 0, s, text, stream_start, pos0, n,
+                                   reinterpret_cast<uint32_t*>(out), count, t.flbase, t.flF, t.flrowout16, t.warm, seg,
+                                   g3);
+                break;
+            case PM_SK_STAGE16:
+                hipLaunchKernelGGL((dfa_sparse_stage16_kernel<88, 4, true>), gs, bs, 0, s, text, stream_start, pos0, n,
+                                   reinterpret_cast<uint32_t*>(out), count, t.sbase8, t.sF, t.sout8, t.sout8h, t.warm,
+                                   seg, g3);
+                break;
+            case PM_SK_STAGE:
+                if (outw == 4)
+                    hipLaunchKernelGGL((dfa_sparse_stage_kernel<4, 16, 1024, false, 4>), gs, bs, 0, s, text,
+                                       stream_start, pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
+                else
+                    hipLaunchKernelGGL((dfa_sparse_stage_kernel<2, 16, 1024, false, 4>), gs, bs, 0, s, text,
+                                       stream_start, pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
+                break;
+            case PM_SK_LOCK8:  // 8-B units, two blocks' text per load; LDS rows for ids only
+                if (outw == 4)
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, 64, 1, 8, 2>), gs, bs, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
+                else if (outw == 2)
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<2, 32, 64, 1, 8, 2>), gs, bs, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
+                else
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<0, 32, 0, 1, 8, 2>), gs, bs, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
+                break;
+            default:  // PM_SK_LOCK16: the 16-B records, register record blocks (no warm-up shortcut)
+                if (outw == 4)
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, 0, 1, 16, 1>), gs, bs, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr);
+                else if (outw == 2)
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<2, 32, 0, 1, 16, 1>), gs, bs, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr);
+                else
+                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<0, 32, 0, 1, 16, 1>), gs, bs, 0, s, text, stream_start,
+                                       pos0, n, out, count, t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr);
+        }
+        return hipGetLastError();
+    }
     int64_t blocks = (nseg + DFA_THREADS * ch - 1) / (DFA_THREADS * ch);
     if (blocks < 1) blocks = 1;
     const dim3 g((unsigned)blocks), b(DFA_THREADS);
-    if (lds_kernel && sdfa_lds >= 25 && t.sbase8 && outw) {
-        // ids staged in LDS (dfa_sparse_stage_kernel): 25 / 26 = 512-lane
-        // workgroups, plain / non-temporal line stores; 27 = 1024-lane
-        // workgroups with 16 rows in LDS; 29-31 = timing ablations of 28
-        const int ST = sdfa_lds >= 27 ? 1024 : 512;
-        int64_t wg = (nseg + ST - 1) / ST;
-        const int64_t cap = lanes / ST;
-        if (wg > cap) wg = cap;
-        if (wg < 1) wg = 1;
-        const dim3 gs((unsigned)wg), bs(ST);
-#define DST4(W)                                                                                                  \
-    hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, 16, 1024, false, 4>), gs, bs, 0, s, text, stream_start, pos0, n, \
-                       out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-#define DST(W, K, T, N)                                                                                             \
-    hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, K, T, N>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, \
-                       t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-        if (sdfa_lds == 26) {
-            if (outw == 4) DST(4, 0, 512, true); else DST(2, 0, 512, true);
-        } else if (sdfa_lds == 27) {
-            if (outw == 4) DST(4, 16, 1024, false); else DST(2, 16, 1024, false);
-        } else if (sdfa_lds == 28) {  // 27 with 4-unit (32-B) record blocks
-            if (outw == 4) DST4(4); else DST4(2);
-        } else if (sdfa_lds >= 35 && sdfa_lds <= 37 && outw == 4) {  // u16 staging rows, 88 / 48 LDS rows (37: plain stores)
-            // (measured and removed: 64-B record blocks here, 5.60 -> 5.84
-            // lines, 3.76 -> 4.12 shipped, 3.80 -> 4.79 ASCII; profiles/r04/gid_order/stage16_blocks64_ab.json)
-            if (!t.sout8h) return hipErrorInvalidValue;
-#define DS16(K, B, N)                                                                                               \
-    hipLaunchKernelGGL((dfa_sparse_stage16_kernel<K, B, N>), gs, bs, 0, s, text, stream_start, pos0, n,                \
-                       reinterpret_cast<uint32_t*>(out), count, t.sbase8, t.sF, t.sout8, t.sout8h, t.warm, seg, g3)
-            // (35: non-temporal whole-line stores, the product -- against
-            // plain ones, 37: lines 5.58 -> 5.45 ms, shipped 3.76 -> 3.56,
-            // ASCII 3.78 -> 3.49; profiles/r04/gid_order/stage16_nt_ab.json.
-            // The output lines no longer evict table lines from L2.)
-            if (sdfa_lds == 35) DS16(88, 4, true);
-            else if (sdfa_lds == 36) DS16(48, 4, true);
-            else DS16(88, 4, false);
-#undef DS16
-        } else if (sdfa_lds >= 34) {  // 28 with the u16 escape table (and 35 / 36 for u16 ids)
-            if (!t.sout8h) return hipErrorInvalidValue;
-#define DSTH(W)                                                                                                     \
-    hipLaunchKernelGGL((dfa_sparse_stage_kernel<W, 16, 1024, false, 4, 0, true>), gs, bs, 0, s, text, stream_start, \
-                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3, t.sout8h)
-            if (outw == 4) DSTH(4); else DSTH(2);
-#undef DSTH
-        } else if (sdfa_lds >= 29 && sdfa_lds <= 31) {  // timing ablations of 28 (u32 ids)
-#define DSTA(A)                                                                                                      \
-    hipLaunchKernelGGL((dfa_sparse_stage_kernel<4, 16, 1024, false, 4, A>), gs, bs, 0, s, text, stream_start, pos0, n, \
-                       out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-            if (outw != 4) return hipErrorInvalidValue;
-            if (sdfa_lds == 29) DSTA(1); else if (sdfa_lds == 30) DSTA(2); else DSTA(3);
-#undef DSTA
-        } else {
-            if (outw == 4) DST(4, 0, 512, false); else DST(2, 0, 512, false);
-        }
-#undef DST
-#undef DST4
-        return hipGetLastError();
-    }
-    if (lds_kernel) {
-        // one workgroup of DFA_LDS_THREADS lanes per CU, persistent over
-        // the segments (the LDS rows are staged once per workgroup)
-        const int lch = sdfa_lds >= 3 && sdfa_lds <= 6 ? 2 : 1;
-        int64_t wg = (nseg + DFA_LDS_THREADS * lch - 1) / (DFA_LDS_THREADS * lch);
-        const int64_t cap = lanes / DFA_LDS_THREADS;
-        if (wg > cap) wg = cap;
-        if (wg < 1) wg = 1;
-        const dim3 g2((unsigned)wg), b2(DFA_LDS_THREADS);
-#define DL(W, B, K, C)                                                                                               \
-    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, K, C>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
-                       t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr)
-#define DL8(W)                                                                                                    \
-    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, 0, 1, 0, 8>), g2, b2, 0, s, text, stream_start, pos0, n, out,  \
-                       count, t.sbase8, t.sF, t.sout8, t.warm, seg, (const uint32_t*)nullptr)
-#define DL8T(W)                                                                                                      \
-    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, 0, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
-                       count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-#define DL8K(W, K)                                                                                                    \
-    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, 32, K, 1, 0, 8, 2>), g2, b2, 0, s, text, stream_start, pos0, n, out, \
-                       count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3)
-#define DLW(W, B, E)                                                                                                 \
-    hipLaunchKernelGGL((dfa_sparse_lds_kernel<W, B, 0, 1, E>), g2, b2, 0, s, text, stream_start, pos0, n, out, count, \
-                       t.sbase, t.sF, t.sout, t.warm, seg, (const uint32_t*)nullptr)
-        switch (sdfa_lds) {
-            case 2:  // the register record blocks alone (timing)
-                if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
-                break;
-            case 3:  // two segments per lane
-                if (outw == 4) DL(4, 16, DFA_LDS_ROWS, 2); else if (outw == 2) DL(2, 16, DFA_LDS_ROWS, 2);
-                else DL(0, 16, DFA_LDS_ROWS, 2);
-                break;
-            case 4:
-                if (outw == 4) DL(4, 32, DFA_LDS_ROWS, 2); else if (outw == 2) DL(2, 32, DFA_LDS_ROWS, 2);
-                else DL(0, 32, DFA_LDS_ROWS, 2);
-                break;
-            case 5:  // record blocks, two segments per lane
-                if (outw == 4) DL(4, 32, 0, 2); else if (outw == 2) DL(2, 32, 0, 2); else DL(0, 32, 0, 2);
-                break;
-            case 6:
-                if (outw == 4) DL(4, 16, 0, 2); else if (outw == 2) DL(2, 16, 0, 2); else DL(0, 16, 0, 2);
-                break;
-            case 7:  // record blocks, 16-position blocks (fewer registers: more waves per SIMD)
-                if (outw == 4) DL(4, 16, 0, 1); else if (outw == 2) DL(2, 16, 0, 1); else DL(0, 16, 0, 1);
-                break;
-            case 9:  // (2) over the 8-B record units (pm_pack_sparse8)
-                if (!t.sbase8) {
-                    if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
-                } else if (outw == 4) DL8(4); else if (outw == 2) DL8(2); else DL8(0);
-                break;
-            case 10:  // (9) with the text of two blocks per load
-                if (!t.sbase8) {
-                    if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
-                } else if (outw == 4) DL8T(4); else if (outw == 2) DL8T(2); else DL8T(0);
-                break;
-            case 11:  // (10) with the first 32 / 64 rows (the root and the shallowest states) in LDS
-            case 12:
-                if (!t.sbase8) {
-                    if (outw == 4) DL(4, 32, 0, 1); else if (outw == 2) DL(2, 32, 0, 1); else DL(0, 32, 0, 1);
-                } else if (sdfa_lds == 11) {
-                    if (outw == 4) DL8K(4, 32); else if (outw == 2) DL8K(2, 32); else DL8K(0, 32);
-                } else {
-                    if (outw == 4) DL8K(4, 64); else if (outw == 2) DL8K(2, 64); else DL8K(0, 64);
-                }
-                break;
-            case 25:  // the staged-id kernels' count only: (10)
-            case 26:
-            case 27:
-            case 28:
-                if (outw == 4) DL8T(4); else if (outw == 2) DL8T(2); else DL8T(0);
-                break;
-            case 22:  // (12) with every block's ids to one line per lane (timing ablation, wrong ids)
-            case 23:  // (12) without escape lookups (timing ablation, wrong ids)
-            case 24:  // (12) with no id stores (timing ablation)
-                if (!t.sbase8 || outw != 4) {
-                    if (outw == 4) DL8T(4); else if (outw == 2) DL8T(2); else DL8T(0);
-                } else if (sdfa_lds == 22) {
-                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, 64, 1, 0, 8, 2, 3>), g2, b2, 0, s, text, stream_start,
-                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
-                } else if (sdfa_lds == 23) {
-                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, 64, 1, 0, 8, 2, 4>), g2, b2, 0, s, text, stream_start,
-                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
-                } else {
-                    hipLaunchKernelGGL((dfa_sparse_lds_kernel<4, 32, 64, 1, 0, 8, 2, 5>), g2, b2, 0, s, text, stream_start,
-                                       pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
-                }
-                break;
-            case 8:  // the same, registers capped for 6 waves per SIMD (three workgroups per CU)
-                if (outw == 4) DLW(4, 16, 6); else if (outw == 2) DLW(2, 16, 6); else DLW(0, 16, 8);
-                break;
-            default:  // 1: LDS rows + record blocks
-                if (outw == 4) DL(4, 32, DFA_LDS_ROWS, 1); else if (outw == 2) DL(2, 32, DFA_LDS_ROWS, 1);
-                else DL(0, 32, DFA_LDS_ROWS, 1);
-        }
-#undef DL
-#undef DLW
-#undef DL8
-#undef DL8T
-#undef DL8K
-        return hipGetLastError();
-    }
-    if (sparse) {
-#define DS(W, C, B)                                                                                           \
-    hipLaunchKernelGGL((dfa_sparse_kernel<W, C, B>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.sbase, \
-                       t.sF, t.sout, t.warm, seg)
-        if (ch == 2) {
-            if (outw == 4 && g_sdfa_blk == 32) DS(4, 2, 32);
-            else if (outw == 4) DS(4, 2, 16); else if (outw == 2) DS(2, 2, 16); else DS(0, 2, 16);
-        } else if (g_sdfa_var && outw == 4) {
-#define DV(V, B)                                                                                                  \
-    hipLaunchKernelGGL((dfa_sparse_kernel<4, 1, B, V>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.sbase, \
-                       t.sF, t.sout, t.warm, seg)
-            switch (g_sdfa_var) {
-                case 1: DV(1, 32); break;
-                case 2: DV(2, 32); break;
-                case 3: DV(3, 32); break;
-                case 4: DV(4, 32); break;
-                case 5: DV(5, 32); break;
-                case 7: DV(7, 32); break;
-                case 12: DV(4, 64); break;
-                case 13: DV(5, 64); break;
-                case 16: DV(8, 32); break;
-                case 32: DV(16, 32); break;
-                case 48: DV(24, 32); break;
-                default: DV(0, 32); break;
-            }
-#undef DV
-        } else if (g_sdfa_blk == 32) {
-            if (outw == 4) DS(4, 1, 32); else if (outw == 2) DS(2, 1, 32); else DS(0, 1, 32);
-        } else {
-            if (outw == 4) DS(4, 1, 16); else if (outw == 2) DS(2, 1, 16); else DS(0, 1, 16);
-        }
-#undef DS
-        return hipGetLastError();
-    }
     if (t.coded) {
-#define DC(W, C) \
-    hipLaunchKernelGGL((dfa_coded_kernel<W, C>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, t.out, t.warm, seg, g3)
-#define DC32(W, C)                                                                                               \
-    hipLaunchKernelGGL((dfa_coded_kernel<W, C, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next, \
-                       t.out, t.warm, seg, g3)
-        if (g_dfa_dense_blk == 32 && outw != 0) {
-            if (ch == 2) {
-                if (outw == 4) DC32(4, 2); else DC32(2, 2);
-            } else {
-                if (outw == 4) DC32(4, 1); else DC32(2, 1);
-            }
-        } else if (ch == 2) {
-            if (outw == 4) DC(4, 2); else if (outw == 2) DC(2, 2); else DC(0, 2);
-        } else {
-            if (outw == 4) DC(4, 1); else if (outw == 2) DC(2, 1); else DC(0, 1);
-        }
-#undef DC
-#undef DC32
+        if (outw == 4)
+            hipLaunchKernelGGL((dfa_coded_kernel<4, 2, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next,
+                               t.out, t.warm, seg, g3);
+        else if (outw == 2)
+            hipLaunchKernelGGL((dfa_coded_kernel<2, 2, 32>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next,
+                               t.out, t.warm, seg, g3);
+        else
+            hipLaunchKernelGGL((dfa_coded_kernel<0, 2>), g, b, 0, s, text, stream_start, pos0, n, out, count, t.next,
+                               t.out, t.warm, seg, g3);
         return hipGetLastError();
     }
     if (outw == 4)
@@ -2713,23 +2408,6 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         hipLaunchKernelGGL(dfa_scan_kernel<0>, g, b, 0, s, text, stream_start, pos0, n, out, count, t, seg);
     return hipGetLastError();
 }
-
-void pm_dfa_set_shape(int lanes_per_cu) {
-    g_dfa_lanes_per_cu = lanes_per_cu > 0 ? lanes_per_cu : DFA_LANES_PER_CU;
-    g_dfa_shape_forced = lanes_per_cu > 0;
-}
-void pm_dfa_set_min_seg(int min_seg) { g_dfa_min_seg = min_seg >= 16 ? min_seg : 0; }
-void pm_dfa_set_sparse(int sparse) { g_dfa_sparse = sparse < 0 ? -1 : sparse != 0; }
-void pm_dfa_set_block(int blk) {
-    g_sdfa_blk = blk == 16 || blk == 32 ? blk : SDFA_BLK;
-    g_dfa_dense_blk = blk == 16 || blk == 32 ? blk : DFA_DENSE_BLK;
-}
-void pm_dfa_set_variant(int v) { g_sdfa_var = v; }
-void pm_dfa_set_lds(int v) { g_sdfa_lds = v >= 0 && v <= 37 ? v : -1; }
-bool pm_dfa_forced_form() { return g_dfa_sparse >= 0; }
-bool pm_dfa_default_sparse() { return g_dfa_sparse != 0; }
-void pm_dfa_set_sync(int on) { g_dfa_sync = on < 0 ? kDfaSyncDefault : on != 0; }
-void pm_dfa_set_chains(int chains) { g_dfa_chains = chains == 1 || chains == 2 ? chains : 0; }
 
 hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n, const uint32_t* parent,
                           const uint32_t* depth, unsigned long long* counts, int num_cu, hipStream_t s) {

@@ -142,6 +142,24 @@ struct StreamSpill {
     uint64_t used = 0;
 };
 
+// Host-path options of an object (pm_hip_set_option; -1 = the environment's
+// default, read once):
+//   host_spin    wait for a read_block slot by polling the stream instead of
+//                hipStreamSynchronize (PM_HOST_SPIN, default 0: no faster)
+//   host_gid16   small read_block_gid calls bring u16 gids over the link and
+//                widen them on the host when every gid < 65,536
+//                (PM_HOST_GID16, default 0: the link wait shrinks 3 us, the
+//                widening costs 5 us more than the copy)
+//   host_events  small calls bracket their launch with timing events for
+//                pm_hip_device_seconds (PM_HOST_SMALL_EVENTS, default 1;
+//                without them a call saves ~2 us of ~40, and the CLI's device
+//                columns report small calls as unmeasured);
+//                profiles/r04/host_path/small_call_variants_ab.json
+//   host_pool    small calls copy / map their results on the process's host
+//                pool (1, default) or on the calling thread alone (0)
+struct HostOpts {
+    int spin = -1, gid16 = -1, events = -1, pool = -1;
+};
 struct PmHip {
     int kind_req = KIND_RT;
     int kind = 0;
@@ -182,7 +200,24 @@ struct PmHip {
     int last_kernel = 0;  // KIND_RT / KIND_AC of the last launch
     int last_out_width = 0;  // bytes per position the last read_block's scans wrote (2 or 4)
     int last_form = 0;    // its DFA form (1 dense rows, 2 sparse; 0 for RT)
+    // per-object options (pm_hip_set_option; the kernel-side ones live in
+    // rt / dfa): the host path's, and the DFA form (0 = timed choice, 1 =
+    // dense rows, 2 = sparse)
+    HostOpts hopt;
+    int dfa_form = 0;
+    uint64_t untimed_calls = 0;  // read_block launches since reset without timing events
+    int last_sparse_kernel = 0;  // PmSparseKernel of the last sparse-form launch (0: none yet)
 };
+
+// Drop the pick's choice and measurements (a measurement still in flight
+// belongs to the old stream: wait for it and drop it).
+void forget_pick(AutoPick& a) {
+    if (a.pending) (void)hipEventSynchronize(a.ev);
+    if (a.timing) (void)hipEventSynchronize(a.t1[a.queue[a.nq - 1]]);
+    a.pending = a.timing = false;
+    a.nq = a.qi = a.trial = 0;
+    a.hold = 0;
+}
 
 void free_pick(AutoPick& a) {
     if (a.d_spill) (void)hipFree(a.d_spill);
@@ -258,7 +293,7 @@ void free_slot(PipeSlot& q) {
 // to their block.  Scratch, not part of the automaton's total_mem.
 void ensure_spill(PmHip* o, uint32_t*& buf, int64_t& cap, int64_t n) {
     if (o->kind != KIND_RT && o->kind != KIND_AUTO) return;
-    const int64_t need = pm_rt_spill_items(n, o->num_cu);
+    const int64_t need = pm_rt_spill_items(n, o->num_cu, o->rt.spill_cap_chunks);
     if (need <= cap) return;
     if (buf) PM_CHECK(hipFree(buf));
     buf = nullptr;
@@ -325,46 +360,31 @@ int host_zero_copy() {
     return z;
 }
 
-// Waiting for a read_block slot by polling the stream (PM_HOST_SPIN=1,
-// pm_hip_debug_host_spin) instead of hipStreamSynchronize.
-int g_host_spin = -1;
-bool host_spin() {
-    if (g_host_spin < 0) {
-        const char* e = std::getenv("PM_HOST_SPIN");
-        g_host_spin = e ? (std::strtol(e, nullptr, 10) != 0) : 0;
-    }
-    return g_host_spin != 0;
-}
-
-// Small (staged) read_block_gid calls: u16 gids over the link, widened on
-// the host, when every gid < 65,536 (PM_HOST_GID16, default 0: the link
-// wait shrinks 3 us, the widening costs 5 us more than the copy), and
-// small calls' launches bracketed by timing events for
-// pm_hip_device_seconds (PM_HOST_SMALL_EVENTS, default 1; without them a
-// call saves ~2 us of ~40 but pm_hip_device_seconds -- the CSV's GPU
-// columns -- leaves small calls out; profiles/r04/host_path/
-// small_call_variants_ab.json).  pm_hip_debug_host_small sets both.
-int g_gid16 = -1, g_small_events = -1;
 int env_int(const char* k, int d) {
     const char* e = std::getenv(k);
     return e ? (int)std::strtol(e, nullptr, 10) : d;
 }
-bool small_gid16() {
-    if (g_gid16 < 0) g_gid16 = env_int("PM_HOST_GID16", 0) != 0;
-    return g_gid16 != 0;
-}
-bool small_events() {
-    if (g_small_events < 0) g_small_events = env_int("PM_HOST_SMALL_EVENTS", 1) != 0;
-    return g_small_events != 0;
+
+bool opt_or_env(int v, const char* env, int d) {
+    if (v >= 0) return v != 0;
+    return env_int(env, d) != 0;
 }
 
 // Host threads for the copy/map work around the pipeline (PM_HOST_THREADS,
-// default min(8, hardware threads)).
+// default min(8, the job's core share)).
+unsigned core_share() {
+    static const unsigned c = [] {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const int omp = env_int("OMP_NUM_THREADS", 0);  // the job's share on a shared host
+        return omp > 0 ? std::min(hw, (unsigned)omp) : hw;
+    }();
+    return c;
+}
 unsigned host_threads() {
     static const unsigned t = [] {
         const char* e = std::getenv("PM_HOST_THREADS");
         long v = e ? std::strtol(e, nullptr, 10) : 0;
-        if (v <= 0) v = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        if (v <= 0) v = std::min(8u, core_share());
         return (unsigned)std::min(v, 64L);
     }();
     return t;
@@ -374,22 +394,31 @@ unsigned host_threads() {
 // calls (the reference's 100 KiB chunks, measure.c:77), whose ~10-27 us of
 // single-threaded host work is a quarter to a half of the call: a thread
 // per piece per call would cost more than the piece.  Workers spin on a
-// ticket for up to PM_HOST_POOL_SPIN_US (default 200) microseconds after
-// their last piece -- so back-to-back calls find them awake -- then sleep
-// on a condition variable.  A job is one generation of the ticket (gen <<
-// 40 | pieces << 20 | next piece); a worker runs a piece only after
-// claiming it by CAS in that generation, so the job's function stays valid
-// while it runs (the caller waits for every piece before returning).
-// PM_HOST_POOL = the workers (default 3; 0 = off: the caller does it all).
+// ticket for up to PM_HOST_POOL_SPIN_US (default 200; 0 when the job's core
+// share is below 8, so the spin never competes with the job's own threads)
+// microseconds after their last piece -- so back-to-back calls find them
+// awake -- then sleep on a condition variable.  A job is one generation of
+// the ticket (gen << 40 | pieces << 20 | next piece); a worker runs a piece
+// only after claiming it by CAS in that generation, so the job's function
+// stays valid while it runs (the caller waits for every piece before
+// returning).  PM_HOST_POOL = the workers (default 3, at most the core share
+// minus one; 0 = no pool).  The pool is a static object: its destructor (at
+// exit or when the library is unloaded) wakes the workers and joins them.
 class HostPool {
 public:
     explicit HostPool(unsigned workers) {
-        const char* e = std::getenv("PM_HOST_POOL_SPIN_US");
-        spin_us_ = e ? std::max(0L, std::strtol(e, nullptr, 10)) : 200L;
-        for (unsigned i = 0; i < workers; ++i) std::thread([this] { loop(); }).detach();
-        workers_ = workers;
+        spin_us_ = std::max(0, env_int("PM_HOST_POOL_SPIN_US", core_share() >= 8 ? 200 : 0));
+        for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
     }
-    unsigned workers() const { return workers_; }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            stop_.store(true, std::memory_order_seq_cst);
+            cv_.notify_all();
+        }
+        for (std::thread& t : th_) t.join();
+    }
+    unsigned workers() const { return (unsigned)th_.size(); }
     // f(k) for k in [0, pieces) on the workers and the caller; returns when all are done
     void run(unsigned pieces, const std::function<void(unsigned)>& f) {
         std::lock_guard<std::mutex> g(submit_);
@@ -425,16 +454,20 @@ private:
     }
     void loop() {
         uint64_t seen = 0;
-        for (;;) {
+        while (!stop_.load(std::memory_order_acquire)) {
             const auto t0 = std::chrono::steady_clock::now();
             uint64_t g;
             unsigned spins = 0;
             while ((g = ticket_.load(std::memory_order_acquire) >> 40) == seen) {
+                if (stop_.load(std::memory_order_acquire)) return;
                 if ((++spins & 1023u) == 0 &&
                     std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
                     std::unique_lock<std::mutex> l(m_);
                     sleepers_.fetch_add(1, std::memory_order_seq_cst);
-                    cv_.wait(l, [&] { return (ticket_.load(std::memory_order_seq_cst) >> 40) != seen; });
+                    cv_.wait(l, [&] {
+                        return stop_.load(std::memory_order_seq_cst) ||
+                               (ticket_.load(std::memory_order_seq_cst) >> 40) != seen;
+                    });
                     sleepers_.fetch_sub(1, std::memory_order_relaxed);
                 }
             }
@@ -444,28 +477,24 @@ private:
     }
     std::atomic<uint64_t> ticket_{0};
     std::atomic<unsigned> pending_{0}, sleepers_{0};
+    std::atomic<bool> stop_{false};
     std::atomic<const std::function<void(unsigned)>*> fn_{nullptr};
     std::mutex submit_, m_;
     std::condition_variable cv_;
     long spin_us_ = 200;
-    unsigned workers_ = 0;
+    std::vector<std::thread> th_;
 };
 
-int g_host_pool = -1;  // workers; -1: PM_HOST_POOL (default 3)
 HostPool* host_pool() {
-    static std::mutex mu;
-    static HostPool* pool = nullptr;  // leaked: its detached workers outlive every object
-    std::lock_guard<std::mutex> g(mu);
-    if (g_host_pool < 0) g_host_pool = std::max(0, std::min(env_int("PM_HOST_POOL", 3), 15));
-    if (g_host_pool == 0) return nullptr;
-    if (!pool) pool = new HostPool((unsigned)g_host_pool);
-    return pool;
+    static HostPool pool((unsigned)std::max(
+        0, std::min({env_int("PM_HOST_POOL", 3), 15, (int)core_share() - 1})));
+    return pool.workers() ? &pool : nullptr;
 }
 
 // f(lo, hi) over [0, n) of a small block: pieces on the pool, or the caller alone.
 template <class F>
-void small_par(size_t n, const F& f) {
-    HostPool* p = n >= ((size_t)16 << 10) ? host_pool() : nullptr;
+void small_par(bool use_pool, size_t n, const F& f) {
+    HostPool* p = use_pool && n >= ((size_t)16 << 10) ? host_pool() : nullptr;
     const unsigned pieces = p ? std::min<unsigned>(p->workers() + 1, (unsigned)(n >> 14)) : 1u;
     if (pieces <= 1) {
         f((size_t)0, n);
@@ -504,14 +533,16 @@ hipError_t launch_cand(PmHip* o, AutoPick& ap, int c, const uint8_t* text, int64
     if (c == CAND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
     DfaDev d = o->dfa;
     d.form = c == CAND_SPARSE ? 2 : 1;
+    o->last_sparse_kernel = pm_dfa_sparse_choice(d, out ? outw : 0);
     return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, d, o->num_cu, s);
 }
 
-// The DFA forms to try, in order (dense rows, then rows + records).
+// The DFA forms to try, in order (dense rows, then rows + records; only the
+// object's forced form when it has one).
 void start_trials(const PmHip* o, AutoPick& ap) {
     ap.nq = 0;
-    ap.queue[ap.nq++] = CAND_DENSE;
-    if (o->dfa.sbase) ap.queue[ap.nq++] = CAND_SPARSE;
+    if (o->dfa_form != 2 || !o->dfa.sbase) ap.queue[ap.nq++] = CAND_DENSE;
+    if (o->dfa.sbase && o->dfa_form != 1) ap.queue[ap.nq++] = CAND_SPARSE;
     ap.qi = 0;
     ap.trial = 0;
 }
@@ -565,11 +596,14 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
     t.spill = spill;
     t.spill_cap = spill_cap;
     if (o->kind == KIND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
-    // one DFA form only (an uncoded automaton), or a form forced for timing
-    if (o->kind == KIND_AC && (!o->dfa.sbase || pm_dfa_forced_form())) {
+    // one DFA form only (an uncoded automaton), or the object's forced form
+    if (o->kind == KIND_AC && (!o->dfa.sbase || o->dfa_form)) {
         ap.last = KIND_AC;
-        ap.last_form = o->dfa.sbase && pm_dfa_forced_form() && pm_dfa_default_sparse() ? 2 : 1;
-        return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, o->dfa, o->num_cu, s);
+        DfaDev d = o->dfa;
+        d.form = o->dfa.sbase ? (o->dfa_form ? o->dfa_form : 2) : 1;
+        ap.last_form = d.form == 2 ? 2 : 1;
+        o->last_sparse_kernel = pm_dfa_sparse_choice(d, out ? outw : 0);
+        return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, d, o->num_cu, s);
     }
     // KIND_AUTO / KIND_AC (see AUTO_SPILL_FRAC): RT launches are measured
     // (spill count and time); a deep one (or, for KIND_AC, the end of a
@@ -635,7 +669,7 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
 // dictionary) come back as u16 gids (half the PCIe bytes) for the host
 // threads to map: +12% (RT) / +28% (AC).  Gids for the caller stay u32 and
 // direct: widening u16 on the host measured 2-5% slower.  Rates: DESIGN.md §5.
-// Host-path breakdown (pm_hip_debug_host_profile): seconds spent staging
+// Host-path breakdown (pm_hip_host_profile): seconds spent staging
 // the input, enqueueing the copies and the launch, waiting for the slot,
 // and copying / mapping the results; calls.
 double g_hprof[5] = {0, 0, 0, 0, 0};
@@ -663,9 +697,12 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         t_mark = t;
     };
     if (g_hprof_on) g_hprof[4] += 1;
+    const bool pool = o->hopt.pool != 0;  // (the pool's size: PM_HOST_POOL)
+    const bool gid16 = opt_or_env(o->hopt.gid16, "PM_HOST_GID16", 0);
+    const bool events = opt_or_env(o->hopt.events, "PM_HOST_SMALL_EVENTS", 1);
     auto finish = [&](PipeSlot& q) {
         lap(1);
-        if (host_spin()) {
+        if (opt_or_env(o->hopt.spin, "PM_HOST_SPIN", 0)) {
             hipError_t e;
             while ((e = hipStreamQuery(q.stream)) == hipErrorNotReady) {}
             PM_CHECK(e);
@@ -682,7 +719,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         if (out_gid && q.staged && q.w == 2) {  // widen
             const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
             uint32_t* dst = out_gid + q.off;
-            small_par(q.m, [&](size_t lo, size_t hi) {
+            small_par(pool, q.m, [&](size_t lo, size_t hi) {
                 for (size_t j = lo; j < hi; ++j) dst[j] = g[j];
             });
         } else if (!out_gid) {
@@ -696,10 +733,10 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
                     for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
                 }
             };
-            if (q.staged) small_par(q.m, map_ids);
+            if (q.staged) small_par(pool, q.m, map_ids);
             else par_range(q.m, (size_t)1 << 18, map_ids);
         } else if (q.staged) {
-            small_par(q.m, [&](size_t lo, size_t hi) {
+            small_par(pool, q.m, [&](size_t lo, size_t hi) {
                 std::memcpy(out_gid + q.off + lo, q.h_res + lo, (hi - lo) * sizeof(uint32_t));
             });
         }
@@ -738,8 +775,9 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             PM_CHECK(hipMemcpyAsync(q.d_stage + ctx, buf + done, m, hipMemcpyHostToDevice, q.stream));
             PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
         }
-        q.w = narrow || (out_gid && q.staged && fits16 && small_gid16()) ? 2 : 4;
-        q.timed = !q.staged || small_events();
+        q.w = narrow || (out_gid && q.staged && fits16 && gid16) ? 2 : 4;
+        q.timed = !q.staged || events;
+        if (!q.timed) o->untimed_calls++;
         if (q.timed) PM_CHECK(hipEventRecord(q.ev0, q.stream));
         PM_CHECK(launch(o, zc_in ? q.h_stage : q.d_stage, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m,
                         zc_out ? q.h_res : q.d_res, q.w, nullptr, q.stream, q.spill, q.spill_cap, q.pick));
@@ -869,6 +907,13 @@ void pm_hip_compile(void* obj) {
                     o->dfa.sout8h = (const uint16_t*)dalloc_copy(o, h.data(), h.size() * 2);
                 }
             }
+            FlImage fl;  // the fallback-linked form (pm_pack_sparse_fl)
+            if (pm_pack_sparse_fl(im.dfa, fl)) {
+                fl.block.resize(fl.block.size() + 16, 0u);  // the last aligned 32-B block
+                o->dfa.flbase = (const uint8_t*)dalloc_copy(o, fl.block.data(), fl.block.size() * 4);
+                o->dfa.flrowout16 = (const uint16_t*)dalloc_copy(o, fl.rowout16.data(), fl.rowout16.size() * 2);
+                o->dfa.flF = fl.F;
+            }
         }
     }
     // read_char's host step keeps the RT image (rt / auto), or the DFA's
@@ -900,7 +945,7 @@ void pm_hip_compile(void* obj) {
     o->compiled = true;
 }
 
-void pm_hip_debug_host_profile(int on, double* out5) {
+void pm_hip_host_profile(int on, double* out5) {
     if (out5)
         for (int k = 0; k < 5; ++k) out5[k] = g_hprof[k];
     for (double& x : g_hprof) x = 0.0;
@@ -943,18 +988,11 @@ void pm_hip_reset(void* obj) {
     o->hist.clear();
     o->host.state_valid = false;
     o->dev_seconds = 0.0;
+    o->untimed_calls = 0;
     // a new stream: the auto kernel choice is measured again, for read_block
-    // slots and scan_device launches alike (a spill count still in flight
-    // belongs to the old stream: wait for it and drop it)
-    auto forget = [](AutoPick& a) {
-        if (a.pending) (void)hipEventSynchronize(a.ev);
-        if (a.timing) (void)hipEventSynchronize(a.t1[a.queue[a.nq - 1]]);
-        a.pending = a.timing = false;
-        a.nq = a.qi = a.trial = 0;
-        a.hold = 0;
-    };
-    forget(o->pick);
-    for (PipeSlot& q : o->slot) forget(q.pick);
+    // slots and scan_device launches alike
+    forget_pick(o->pick);
+    for (PipeSlot& q : o->slot) forget_pick(q.pick);
 }
 
 void pm_hip_free(void* obj) {
@@ -1106,7 +1144,7 @@ size_t pm_hip_scratch_bytes(void* obj) {
 
 int pm_hip_hold_choice(void* obj, int launches) {
     PmHip* o = as(obj);
-    if (o->kind == KIND_RT || (o->kind == KIND_AC && (!o->dfa.sbase || pm_dfa_forced_form()))) return 0;
+    if (o->kind == KIND_RT || (o->kind == KIND_AC && (!o->dfa.sbase || o->dfa_form))) return 0;
     AutoPick& ap = o->pick;
     resolve_pick(o, ap);
     if (ap.pending || ap.timing || ap.hold <= 0) return -1;
@@ -1125,41 +1163,60 @@ uint32_t pm_hip_parent_gid(void* obj, uint32_t gid) {
 }
 
 // Timing-only ablation launches of the RT kernel (bench_variants.py).
-int pm_hip_debug_scan_variant(void* obj, int variant, const uint8_t* d_text, int64_t n, void* d_out, int out_width,
-                              unsigned long long* d_count, void* hip_stream) {
+int pm_hip_streaming_floor_device(void* obj, const uint8_t* d_text, int64_t n, void* d_out, int out_width,
+                                  void* hip_stream) {
     PmHip* o = as(obj);
     if (o->kind != KIND_RT && o->kind != KIND_AUTO) return -1;
     ensure_spill(o, o->spill, o->spill_cap, n);
     RtDev t = o->rt;
     t.spill = o->spill;
     t.spill_cap = o->spill_cap;
-    hipError_t e = pm_launch_rt_variant(variant, d_text, 0, 0, n, d_out, out_width, d_count, t, o->num_cu,
-                                        (hipStream_t)hip_stream);
+    hipError_t e = pm_launch_rt_floor(d_text, n, d_out, out_width, t, o->num_cu, (hipStream_t)hip_stream);
     return e == hipSuccess ? 0 : -3;
 }
 
-void pm_hip_debug_dfa_chains(int chains) { pm_dfa_set_chains(chains); }
-
-void pm_hip_debug_dfa_sparse(int sparse) { pm_dfa_set_sparse(sparse); }
-void pm_hip_debug_dfa_block(int blk) { pm_dfa_set_block(blk); }
-void pm_hip_debug_dfa_variant(int v) { pm_dfa_set_variant(v); }
-void pm_hip_debug_dfa_lds(int v) { pm_dfa_set_lds(v); }
-void pm_hip_debug_dfa_sync(int on) { pm_dfa_set_sync(on); }
-void pm_hip_debug_spill_cap(int chunks) { pm_rt_set_spill_cap(chunks); }
-void pm_hip_debug_rt_blocks(int b) { pm_rt_set_max_blocks(b); }
-void pm_hip_debug_rt_small(int64_t n) { pm_rt_set_small_max(n); }
-void pm_hip_debug_rt_small_stage(int on) { pm_rt_set_small_stage(on); }
-void pm_hip_debug_host_spin(int on) { g_host_spin = on < 0 ? -1 : on != 0; }
-void pm_hip_debug_host_pool(int workers) {
-    // a pool once made keeps its workers; 0 turns its use off, > 0 back on
-    g_host_pool = workers < 0 ? -1 : workers;
+int pm_hip_set_option(void* obj, const char* name, int64_t value) {
+    PmHip* o = as(obj);
+    if (!name) return -1;
+    const std::string k(name);
+    auto flag = [&](int& dst) {  // -1 = the environment's default, 0 / 1
+        if (value < -1 || value > 1) return -1;
+        dst = (int)value;
+        return 0;
+    };
+    if (k == "dfa_form") {
+        if (value < 0 || value > 2) return -1;
+        o->dfa_form = (int)value;
+        forget_pick(o->pick);  // the choice is measured again
+        for (PipeSlot& q : o->slot) forget_pick(q.pick);
+        return 0;
+    }
+    if (k == "sparse_kernel") {
+        if (value < PM_SK_PRODUCT || value > PM_SK_LOCK16) return -1;
+        o->dfa.sparse_kernel = (int)value;
+        return 0;
+    }
+    if (k == "dfa_sync") {
+        if (value < 0 || value > 1) return -1;
+        o->dfa.sync = (int)value;
+        return 0;
+    }
+    if (k == "rt_small_max") {
+        if (value < -1) return -1;
+        o->rt.small_max = value;
+        return 0;
+    }
+    if (k == "spill_cap_chunks") {
+        if (value < 0 || value > 16) return -1;
+        o->rt.spill_cap_chunks = value;
+        return 0;
+    }
+    if (k == "host_spin") return flag(o->hopt.spin);
+    if (k == "host_gid16") return flag(o->hopt.gid16);
+    if (k == "host_events") return flag(o->hopt.events);
+    if (k == "host_pool") return flag(o->hopt.pool);
+    return -1;
 }
-void pm_hip_debug_host_small(int gid16, int events) {
-    g_gid16 = gid16 < 0 ? -1 : gid16 != 0;
-    g_small_events = events < 0 ? -1 : events != 0;
-}
-void pm_hip_debug_dfa_shape(int lanes_per_cu) { pm_dfa_set_shape(lanes_per_cu); }
-void pm_hip_debug_dfa_min_seg(int min_seg) { pm_dfa_set_min_seg(min_seg); }
 
 int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
                              void* hip_stream) {
@@ -1253,7 +1310,11 @@ uint32_t pm_hip_gid_index(void* obj, uint32_t gid) {
 int pm_hip_kernel_kind(void* obj) { return as(obj)->kind; }
 int pm_hip_kernel_last(void* obj) { return as(obj)->last_kernel; }
 int pm_hip_dfa_form_last(void* obj) { return as(obj)->last_form; }
-double pm_hip_device_seconds(void* obj) { return as(obj)->dev_seconds; }
+int pm_hip_sparse_kernel_last(void* obj) { return as(obj)->last_sparse_kernel; }
+double pm_hip_device_seconds(void* obj) {
+    const PmHip* o = as(obj);
+    return o->untimed_calls ? -1.0 : o->dev_seconds;
+}
 int pm_hip_last_out_width(void* obj) { return as(obj)->last_out_width; }
 double pm_hip_hbm_peak_gbs(void) { return PM_HBM_PEAK_GBS; }
 size_t pm_hip_table_bytes(void* obj) { return as(obj)->table_bytes; }
@@ -1268,6 +1329,8 @@ struct PmFlatHandle {
     DfaImage dfa;
     PmParents par;
     std::vector<uint32_t> block8, out8;  // pm_pack_sparse8 of the DFA's sparse form
+    FlImage fl;                          // pm_pack_sparse_fl of it
+    bool has_fl = false;
     int kind = 0;
     bool hit = false;
 };
@@ -1287,6 +1350,7 @@ void* pm_flat_build_cached(const char* const* pats, const uint32_t* lens, size_t
     h->dfa = std::move(im.dfa);
     h->par = std::move(im.par);
     if (!pm_pack_sparse8(h->dfa, h->block8, h->out8)) h->block8.clear(), h->out8.clear();
+    h->has_fl = pm_pack_sparse_fl(h->dfa, h->fl);
     return h;
 }
 
@@ -1319,6 +1383,8 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
     if (s == "sout") return ret(h->dfa.sout);
     if (s == "sblock8") return ret(h->block8);
     if (s == "sout8") return ret(h->out8);
+    if (s == "flblock") return ret(h->fl.block);
+    if (s == "flrowout16") return ret(h->fl.rowout16);
     if (s == "index_of_gid") return ret(h->g.index_of_gid);
     if (s == "parent") return ret(h->par.parent);
     if (s == "depth") return ret(h->par.depth);
@@ -1329,9 +1395,19 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
 
 // read_char's host step (pm_hoststep.h) over a whole text from the stream
 // start: the RT walk (kind 1), or the DFA step (kind 2; its sparse form, or
-// dense rows when dense_rows is set or it has no sparse form).  CPU tests.
+// dense rows when dense_rows is 1 or it has no sparse form; dense_rows 2:
+// the fallback-linked form's host reference, pm_fl_host_step).  CPU tests.
 int pm_flat_host_scan(void* handle, const uint8_t* text, size_t n, uint32_t* out_gid, int dense_rows) {
     PmFlatHandle* h = static_cast<PmFlatHandle*>(handle);
+    if (h->kind == 2 && dense_rows == 2) {
+        if (!h->has_fl) return -1;
+        uint32_t w = 0;
+        for (size_t k = 0; k < n; ++k) {
+            w = pm_fl_host_step(h->fl, w, text[k], nullptr);
+            out_gid[k] = pm_fl_output(h->fl, w);
+        }
+        return 0;
+    }
     PmHostStep st;
     uint32_t max_len = 0;
     if (h->kind == 1) {

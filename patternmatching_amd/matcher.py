@@ -167,6 +167,11 @@ class HipMatcher:
             self.lib.pm_hip_free(self.obj)
             self.obj = None
 
+    def set_option(self, name: str, value: int) -> int:
+        """pm_hip_set_option: a per-object option (include/pm_hip.h lists
+        them); 0 on success, -1 for an unknown name or value."""
+        return self.lib.pm_hip_set_option(self.obj, name.encode(), int(value))
+
     # --- batch ---------------------------------------------------------
     def read_block_gids(self, data) -> np.ndarray:
         arr = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray)
@@ -250,6 +255,12 @@ class HipMatcher:
     def dfa_form_last(self):
         """1 = dense rows, 2 = rows + records (pm_flatten.h), 0 = RT ran."""
         return self.lib.pm_hip_dfa_form_last(self.obj)
+
+    @property
+    def sparse_kernel_last(self):
+        """The sparse form's kernel of the last launch that ran it
+        ("sparse_kernel" numbering, 0 before any)."""
+        return self.lib.pm_hip_sparse_kernel_last(self.obj)
 
     @property
     def kernel_last(self):

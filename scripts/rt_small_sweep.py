@@ -29,7 +29,7 @@ for stream in ("ascii", "lines"):
     for n in (16 << 10, 100 << 10, 256 << 10, 1 << 20, 4 << 20, N - 4096):
         outs, ts = {}, {}
         for mode, lim in (("chunked", 0), ("small", 1 << 40)):
-            lib.pm_hip_debug_rt_small(lim)
+            m.set_option("rt_small_max", lim)
             o = torch.zeros(n, dtype=torch.int32, device="cuda")
             t = []
             for r in range(12):
@@ -41,7 +41,7 @@ for stream in ("ascii", "lines"):
                 if r >= 2:
                     t.append(e0.elapsed_time(e1) * 1e3)
             outs[mode], ts[mode] = o, statistics.median(t)
-        lib.pm_hip_debug_rt_small(-1)
+        m.set_option("rt_small_max", -1)
         assert torch.equal(outs["chunked"], outs["small"]), (stream, n)
         res[f"{stream}-{n}"] = {"chunked_us": round(ts["chunked"], 2), "small_us": round(ts["small"], 2)}
 print(json.dumps(res, indent=1))

@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
-"""Side by side, one process: the sparse AC-DFA form's kernels (0 = plain
-dfa_sparse_kernel, 1 = LDS rows + register record blocks, 2 = record blocks
-only) on 1 GiB of each stream, dense u32 / u16 / count; ids checked equal.
-Prints one JSON object."""
+"""Side by side, one process: the sparse AC-DFA form's kernels (the
+per-object "sparse_kernel" option, include/pm_hip.h: 1 fallback-linked,
+2 u16-staged 8-B units, 3 u32-staged, 4 lock-step 8-B units, 5 lock-step
+16-B records) on 1 GiB of each stream, ids checked equal across kernels.
+With PM_LIBPM naming another build of the library (scripts/build_ab.sh, e.g.
+an ablation build with -DPM_FL_SPEC=0) the same for that build: run it once
+per build (scripts/ab_libs.sh alternates them).  Prints one JSON object."""
 import argparse
 import json
 import os
@@ -20,9 +23,8 @@ ap.add_argument("--dict", default="snort")
 ap.add_argument("--bytes", type=int, default=1 << 30)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--streams", default="lines,ship,ascii")
-ap.add_argument("--variants", default="0,1,2")
+ap.add_argument("--kernels", default="1,2")
 ap.add_argument("--modes", default="dense")
-ap.add_argument("--nocheck", default="", help="timing ablations whose ids are not checked")
 args = ap.parse_args()
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 WIDTH = {"dense": 4, "dense16": 2, "count": 0}
@@ -32,13 +34,13 @@ d = pm.Dictionary([os.path.join(data, x) for x in DICTS[args.dict]])
 m = pm.HipMatcher("ac")
 m.add_dictionary(d)
 m.compile()
-lib.pm_hip_debug_dfa_sparse(1)  # the sparse form on every launch
+assert m.set_option("dfa_form", 2) == 0  # the sparse form on every launch
 n = args.bytes
 s = torch.cuda.current_stream()
 text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
 outs = {w: torch.empty(n * max(w, 1) // 4 + 16, dtype=torch.int32, device="cuda") for w in (4, 2)}
 cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-res = {}
+res = {"lib": os.environ.get("PM_LIBPM", "libpm.so"), "dict": args.dict, "bytes": n}
 for st in args.streams.split(","):
     if st == "lines":
         m.gen_lines_device(text.data_ptr(), n + 64, 1, s.cuda_stream)
@@ -49,13 +51,14 @@ for st in args.streams.split(","):
         lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, 1, 0 if st == "ascii" else 1, s.cuda_stream)
     for mode in args.modes.split(","):
         w = WIDTH[mode]
-        vs = [int(v) for v in args.variants.split(",")]
-        times = {v: [] for v in vs}
+        ks = [int(v) for v in args.kernels.split(",")]
+        times = {k: [] for k in ks}
+        ran = {}
         ref = None
         counts = {}
         for r in range(args.rounds + 1):
-            for v in vs:
-                lib.pm_hip_debug_dfa_lds(v)
+            for k in ks:
+                assert m.set_option("sparse_kernel", k) == 0
                 cnt.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
@@ -63,19 +66,19 @@ for st in args.streams.split(","):
                               s.cuda_stream, out_width=w or 4)
                 e1.record(s)
                 torch.cuda.synchronize()
+                ran[k] = m.sparse_kernel_last
                 if r:
-                    times[v].append(e0.elapsed_time(e1))
-                counts[v] = int(cnt.item())
-                if r == 0 and w and str(v) not in args.nocheck.split(","):
-                    h = int(outs[w][: n * w // 4].view(torch.int64)[:: 997].sum().item())
+                    times[k].append(e0.elapsed_time(e1))
+                counts[k] = int(cnt.item())
+                if r == 0 and w:
                     if ref is None:
-                        ref = (h, outs[w][: n * w // 4].clone())
-                    elif not torch.equal(ref[1], outs[w][: n * w // 4]):
-                        raise SystemExit(f"{st} {mode}: variant {v} ids differ from variant {vs[0]}")
+                        ref = outs[w][: n * w // 4].clone()
+                    elif not torch.equal(ref, outs[w][: n * w // 4]):
+                        raise SystemExit(f"{st} {mode}: kernel {k} ids differ from kernel {ks[0]}")
         del ref
-        assert len({c for v, c in counts.items() if str(v) not in args.nocheck.split(",")}) <= 1, counts
-        for v in vs:
-            ms = statistics.median(times[v])
-            res[f"{st}-{mode}-v{v}"] = {"ms": round(ms, 4), "stream_gbps": round(n / ms / 1e6, 1),
-                                       "matches": counts[v]}
+        assert len(set(counts.values())) <= 1, counts
+        for k in ks:
+            ms = statistics.median(times[k])
+            res[f"{st}-{mode}-k{k}"] = {"ms": round(ms, 4), "stream_gbps": round(n / ms / 1e6, 1),
+                                       "matches": counts[k], "ran": ran[k]}
 print(json.dumps(res))

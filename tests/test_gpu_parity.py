@@ -37,6 +37,7 @@ def matcher(key, kind):
         _m[(key, kind)] = m
     m = _m[(key, kind)]
     m.reset()
+    m.set_option("rt_small_max", _RT_SMALL[0])
     return m
 
 
@@ -181,18 +182,20 @@ def test_duplicate_add_pattern_last_id_wins(kind):
     m.free()
 
 
-@pytest.fixture(params=["chunked", "small", "small_lds"])
+_RT_SMALL = [-1]  # the "rt_small_max" option matcher() applies
+
+
+@pytest.fixture(params=["chunked", "small"])
 def rt_small(request):
     """RT launches of small sizes through the chunked kernel or the
-    one-thread-per-position kernel (pm_hip_debug_rt_small), reading the text
-    where it lies (the default) or with its text window staged in LDS
-    (pm_hip_debug_rt_small_stage); all exact."""
-    lib = pm.load()
-    lib.pm_hip_debug_rt_small(0 if request.param == "chunked" else 1 << 40)
-    lib.pm_hip_debug_rt_small_stage(1 if request.param == "small_lds" else 0)
-    yield request.param
-    lib.pm_hip_debug_rt_small(-1)
-    lib.pm_hip_debug_rt_small_stage(0)
+    one-thread-per-position kernel (the per-object "rt_small_max" option:
+    0 = never, 2^40 = every launch); all exact.  Yields the option value for
+    matchers a test makes itself; matcher() applies it to the cached ones."""
+    _RT_SMALL[0] = 0 if request.param == "chunked" else 1 << 40
+    yield _RT_SMALL[0]
+    _RT_SMALL[0] = -1
+    for m in _m.values():
+        m.set_option("rt_small_max", -1)
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -215,6 +218,7 @@ def test_kmp_kat(kind, rt_small):
     m = pm.HipMatcher(kind)
     m.add_dictionary(d)
     m.compile()
+    m.set_option("rt_small_max", rt_small)
     codes = m.read_block_codes(np.fromfile(os.path.join(DATA, "kmp_kat.stream"), dtype=np.uint8))
     assert list(np.nonzero(codes)[0]) == [17, 42]
     m.free()
@@ -241,6 +245,7 @@ def test_edge_dictionaries_brute_force(name, kind, rt_small):
     m = pm.HipMatcher(kind)
     m.add_dictionary(d)
     m.compile()
+    m.set_option("rt_small_max", rt_small)
     rng = np.random.default_rng(9)
     alphabet = np.unique(np.frombuffer(b"".join(pats), np.uint8))
     text = rng.choice(alphabet, size=20000).astype(np.uint8)
@@ -416,10 +421,9 @@ def test_small_gid_calls_u16_and_u32(kind, key):
     """Small read_block_gid calls (<= 256 Ki positions) bring u16 gids over
     the link and widen them on the host when every gid fits, u32 otherwise
     (a 70,000-pattern dictionary), with or without the per-call timing
-    events (pm_hip_debug_host_small), their results copied / mapped on the
-    host pool or by the caller alone (pm_hip_debug_host_pool): every form
-    equals one large call, for gids and pattern ids."""
-    lib = pm.load()
+    events (the "host_gid16" / "host_events" options), their results
+    copied / mapped on the host pool or by the caller alone ("host_pool"):
+    every form equals one large call, for gids and pattern ids."""
     if key == "snort":
         m = matcher("snort", kind)
         text = np.tile(SHIP, 1 + (600 << 10) // len(SHIP))[:600 << 10]
@@ -438,8 +442,8 @@ def test_small_gid_calls_u16_and_u32(kind, key):
     whole_ids = m.read_block_id_array(text)
     try:
         for gid16, ev, pool in ((1, 0, -1), (0, 0, -1), (1, 1, -1), (0, 1, 0), (1, 0, 0)):
-            lib.pm_hip_debug_host_small(gid16, ev)
-            lib.pm_hip_debug_host_pool(pool)  # the result copy / id map on the host pool, or not
+            assert m.set_option("host_gid16", gid16) == 0 and m.set_option("host_events", ev) == 0
+            assert m.set_option("host_pool", pool) == 0  # the result copy / id map on the host pool, or not
             m.reset()
             parts = [m.read_block_gids(text[o:o + (100 << 10)]) for o in range(0, len(text), 100 << 10)]
             assert np.array_equal(np.concatenate(parts), whole), (gid16, ev, pool)
@@ -447,8 +451,8 @@ def test_small_gid_calls_u16_and_u32(kind, key):
             ids = [m.read_block_id_array(text[o:o + (100 << 10)]) for o in range(0, len(text), 100 << 10)]
             assert np.array_equal(np.concatenate(ids), whole_ids), (gid16, ev, pool)
     finally:
-        lib.pm_hip_debug_host_small(-1, -1)
-        lib.pm_hip_debug_host_pool(-1)
+        for k in ("host_gid16", "host_events", "host_pool"):
+            m.set_option(k, -1)
     if key == "70k":
         m.free()
 
@@ -654,16 +658,15 @@ def test_full_size_binary_and_deep_streams_kernels_agree(stream):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert int(ca.item()) == int(cb.item()) == int((a != 0).sum().item())
-    lib = pm.load()
     try:  # both DFA forms at full size
-        for form in (0, 1):
-            lib.pm_hip_debug_dfa_sparse(form)
+        for form in (1, 2):
+            ac.set_option("dfa_form", form)
             b.zero_()
             ac.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), None, s)
             torch.cuda.synchronize()
-            assert ac.dfa_form_last == 1 + form and torch.equal(a, b), form
+            assert ac.dfa_form_last == form and torch.equal(a, b), form
     finally:
-        lib.pm_hip_debug_dfa_sparse(-1)
+        ac.set_option("dfa_form", 0)
     for _ in range(2):  # auto: an RT launch, then (deep stream) the DFA
         b.zero_()
         au.scan_device(dt.data_ptr(), 0, 0, n, b.data_ptr(), None, s)
@@ -765,10 +768,9 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
         for size, start in ((n, 0), (1000, 5000), (100 << 10, 12345), (3 << 20, 1 << 20)):
             start &= ~15
             got = {}
-            for sparse, blk, sync in [(x, b, y) for x in (0, 1) for b in (16, 32) for y in (0, 1)]:
-                lib.pm_hip_debug_dfa_sparse(sparse)
-                lib.pm_hip_debug_dfa_block(blk)
-                lib.pm_hip_debug_dfa_sync(sync)
+            for form, sync in [(x, y) for x in (1, 2) for y in (0, 1)]:
+                ac.set_option("dfa_form", form)
+                ac.set_option("dfa_sync", sync)
                 a = torch.zeros(size, dtype=torch.int32, device="cuda")
                 h = torch.zeros(size, dtype=torch.int16, device="cuda")
                 c = torch.zeros(3, dtype=torch.int64, device="cuda")
@@ -776,8 +778,8 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
                 ac.scan_device(dt.data_ptr(), 0, start, size, h.data_ptr(), c[1:2].data_ptr(), s, out_width=2)
                 ac.scan_device(dt.data_ptr(), 0, start, size, 0, c[2:3].data_ptr(), s)
                 torch.cuda.synchronize()
-                got[(sparse, blk, sync)] = (a, h, c)
-            a0, h0, c0 = got[(0, 16, 0)]
+                got[(form, sync)] = (a, h, c)
+            a0, h0, c0 = got[(1, 0)]
             for key in list(got)[1:]:
                 a1, h1, c1 = got[key]
                 assert torch.equal(a0, a1) and torch.equal(h0, h1) and torch.equal(c0, c1), key
@@ -785,22 +787,24 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
             assert int(c1[0].item()) == int(c1[2].item()) == int((a1 != 0).sum().item())
             assert torch.equal(h1.to(torch.int32) & 0xFFFF, a1)
     finally:
-        lib.pm_hip_debug_dfa_sparse(-1)
-        lib.pm_hip_debug_dfa_block(0)
-        lib.pm_hip_debug_dfa_sync(-1)
+        ac.set_option("dfa_form", 0)
+        ac.set_option("dfa_sync", 1)
+
+
+# the sparse form's kernels ("sparse_kernel" option) and the widths each writes
+SPARSE_KERNELS = {1: (4,), 2: (4,), 3: (4, 2), 4: (4, 2, 0), 5: (4, 2, 0)}
 
 
 @pytest.mark.parametrize("stream", ["lines", "ship"])
 def test_sparse_dfa_kernel_variants_agree(stream):
-    """Every kernel of the sparse form (pm_hip_debug_dfa_lds 0-12, 25-27:
-    plain, LDS rows, register record blocks, two segments per lane,
-    16-position blocks, capped registers, 8-B units, ids staged in LDS and
-    stored as whole lines)
-    at 512 / 1024 / 1536 lanes per CU gives the RT
-    kernel's u32 / u16 ids and the same count, at sizes from one warm-up
-    segment to 32 MiB (snort)."""
+    """Every product kernel of the sparse form ("sparse_kernel" 1-5: the
+    fallback-linked form, the u16- and u32-staged 8-B-unit kernels, the
+    lock-step kernels over 8-B units and 16-B records), under both warm-up
+    rules, gives the RT kernel's u32 / u16 ids and the same count, at sizes
+    from one warm-up segment to 32 MiB (snort); a width a kernel does not
+    write runs the product choice, and pm_hip_sparse_kernel_last says which
+    ran."""
     torch = _torch()
-    lib = pm.load()
     rt, ac = matcher("snort", "rt"), matcher("snort", "ac")
     n = 32 << 20
     s = torch.cuda.current_stream().cuda_stream
@@ -811,31 +815,29 @@ def test_sparse_dfa_kernel_variants_agree(stream):
         dt.copy_(torch.from_numpy(np.tile(SHIP, (n + 64) // len(SHIP) + 1)[: n + 64]).cuda())
     ref = torch.empty(n, dtype=torch.int32, device="cuda")
     rt.scan_device(dt.data_ptr(), 0, 0, n, ref.data_ptr(), None, s)
-    lib.pm_hip_debug_dfa_sparse(1)
+    ac.set_option("dfa_form", 2)
     try:
         for size, start in ((n, 0), (777, 4096), (100 << 10, 12345 & ~15), (5 << 20, 3 << 20)):
-            for form, lanes, sync in [(f, ln, y) for f in list(range(13)) + [25, 26, 27, 28, 34, 35, 36, 37]
-                                      for ln in ((512, 1024, 1536) if f in (2, 8, 9, 10, 12, 25, 27, 28) else (0,))
-                                      for y in ((0, 1) if f in (10, 11, 12, 25, 27, 28, 34, 35) else (0,))]:
-                    lib.pm_hip_debug_dfa_lds(form)
-                    lib.pm_hip_debug_dfa_shape(lanes)
-                    lib.pm_hip_debug_dfa_sync(sync)
-                    a = torch.zeros(size, dtype=torch.int32, device="cuda")
-                    h = torch.zeros(size, dtype=torch.int16, device="cuda")
-                    c = torch.zeros(2, dtype=torch.int64, device="cuda")
-                    ac.scan_device(dt.data_ptr(), 0, start, size, a.data_ptr(), c[0:1].data_ptr(), s)
-                    ac.scan_device(dt.data_ptr(), 0, start, size, h.data_ptr(), None, s, out_width=2)
-                    ac.scan_device(dt.data_ptr(), 0, start, size, 0, c[1:2].data_ptr(), s)
-                    torch.cuda.synchronize()
-                    tag = (size, form, lanes, sync)
-                    assert torch.equal(a, ref[start:start + size]), tag
-                    assert torch.equal(h.to(torch.int32) & 0xFFFF, a), tag
-                    assert int(c[0].item()) == int(c[1].item()) == int((a != 0).sum().item()), tag
+            for sk, sync in [(k, y) for k in SPARSE_KERNELS for y in (0, 1)]:
+                assert ac.set_option("sparse_kernel", sk) == 0 and ac.set_option("dfa_sync", sync) == 0
+                a = torch.zeros(size, dtype=torch.int32, device="cuda")
+                h = torch.zeros(size, dtype=torch.int16, device="cuda")
+                c = torch.zeros(2, dtype=torch.int64, device="cuda")
+                tag = (size, sk, sync)
+                ac.scan_device(dt.data_ptr(), 0, start, size, a.data_ptr(), c[0:1].data_ptr(), s)
+                assert ac.sparse_kernel_last == sk, tag
+                ac.scan_device(dt.data_ptr(), 0, start, size, h.data_ptr(), None, s, out_width=2)
+                assert (ac.sparse_kernel_last == sk) == (2 in SPARSE_KERNELS[sk]), tag
+                ac.scan_device(dt.data_ptr(), 0, start, size, 0, c[1:2].data_ptr(), s)
+                assert (ac.sparse_kernel_last == sk) == (0 in SPARSE_KERNELS[sk]), tag
+                torch.cuda.synchronize()
+                assert torch.equal(a, ref[start:start + size]), tag
+                assert torch.equal(h.to(torch.int32) & 0xFFFF, a), tag
+                assert int(c[0].item()) == int(c[1].item()) == int((a != 0).sum().item()), tag
     finally:
-        lib.pm_hip_debug_dfa_lds(-1)
-        lib.pm_hip_debug_dfa_shape(0)
-        lib.pm_hip_debug_dfa_sync(-1)
-        lib.pm_hip_debug_dfa_sparse(-1)
+        ac.set_option("sparse_kernel", 0)
+        ac.set_option("dfa_sync", 1)
+        ac.set_option("dfa_form", 0)
 
 
 @pytest.mark.parametrize("stream", ["lines", "ship"])
@@ -845,10 +847,9 @@ def test_dfa_warmups_stop_at_stream_start(stream):
     dfa_sync_lo) must not look at them.  The bytes before stream_start are
     pattern-dense text of another seed, stream_start is not aligned, and the
     first positions lie within max_len of it; every DFA form (dense rows;
-    sparse plain / record blocks / 8-B units / LDS rows) under both warm-up
-    rules gives the RT kernel's u32 / u16 ids and count."""
+    every kernel of the sparse form) under both warm-up rules gives the RT
+    kernel's u32 / u16 ids and count."""
     torch = _torch()
-    lib = pm.load()
     rt, ac = matcher("snort", "rt"), matcher("snort", "ac")
     n = 4 << 20
     s = torch.cuda.current_stream().cuda_stream
@@ -866,11 +867,11 @@ def test_dfa_warmups_stop_at_stream_start(stream):
             buf[stream_start:] = dt[: n + 64 - stream_start]
             ref = torch.empty(size, dtype=torch.int32, device="cuda")
             rt.scan_device(buf.data_ptr(), stream_start, pos0, size, ref.data_ptr(), None, s)
-            forms = [(0, -1, y) for y in (0, 1)] + [(1, f, y) for f in (0, 2, 10, 12, 25, 27, 28, 34, 35) for y in (0, 1)]
-            for sparse, lds, sync in forms:
-                lib.pm_hip_debug_dfa_sparse(sparse)
-                lib.pm_hip_debug_dfa_lds(lds)
-                lib.pm_hip_debug_dfa_sync(sync)
+            forms = [(1, 0, y) for y in (0, 1)] + [(2, k, y) for k in [0] + list(SPARSE_KERNELS) for y in (0, 1)]
+            for form, sk, sync in forms:
+                ac.set_option("dfa_form", form)
+                ac.set_option("sparse_kernel", sk)
+                ac.set_option("dfa_sync", sync)
                 a = torch.zeros(size, dtype=torch.int32, device="cuda")
                 h = torch.zeros(size, dtype=torch.int16, device="cuda")
                 c = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -878,14 +879,14 @@ def test_dfa_warmups_stop_at_stream_start(stream):
                 ac.scan_device(buf.data_ptr(), stream_start, pos0, size, h.data_ptr(), None, s, out_width=2)
                 ac.scan_device(buf.data_ptr(), stream_start, pos0, size, 0, c.data_ptr(), s)
                 torch.cuda.synchronize()
-                tag = (stream_start, pos0, sparse, lds, sync)
+                tag = (stream_start, pos0, form, sk, sync)
                 assert torch.equal(a, ref), tag
                 assert torch.equal(h.to(torch.int32) & 0xFFFF, a), tag
                 assert int(c.item()) == int((a != 0).sum().item()), tag
     finally:
-        lib.pm_hip_debug_dfa_lds(-1)
-        lib.pm_hip_debug_dfa_sync(-1)
-        lib.pm_hip_debug_dfa_sparse(-1)
+        ac.set_option("sparse_kernel", 0)
+        ac.set_option("dfa_sync", 1)
+        ac.set_option("dfa_form", 0)
 
 
 def test_adversarial_stream_large_rt_equals_ac():
@@ -1006,7 +1007,7 @@ def test_bounded_spill_region_resolves_many_times(cap):
     want = torch.empty(n, dtype=torch.int32, device="cuda")
     matcher("merged", "ac").scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s)
     rt = matcher("merged", "rt")
-    lib.pm_hip_debug_spill_cap(cap)
+    rt.set_option("spill_cap_chunks", cap)
     try:
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         got16 = torch.empty(n, dtype=torch.int16, device="cuda")
@@ -1016,7 +1017,7 @@ def test_bounded_spill_region_resolves_many_times(cap):
         rt.scan_device(dt.data_ptr(), 0, 0, n, None, c[2:].data_ptr(), s)
         torch.cuda.synchronize()
     finally:
-        lib.pm_hip_debug_spill_cap(0)
+        rt.set_option("spill_cap_chunks", 0)
     assert torch.equal(got, want)
     assert torch.equal(got16.to(torch.int32) & 0xFFFF, want)
     nz = int((want != 0).sum().item())
@@ -1038,17 +1039,16 @@ def test_rt_scan_device_concurrent_streams_spill():
     want = torch.empty(n, dtype=torch.int32, device="cuda")
     ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    lib = pm.load()
-    lib.pm_hip_debug_spill_cap(2)
+    m = matcher("et", "rt")
+    m.set_option("spill_cap_chunks", 2)
     try:
-        m = matcher("et", "rt")
         streams = [torch.cuda.Stream() for _ in range(6)]
         outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(18)]
         for k, o in enumerate(outs):
             m.scan_device(dt.data_ptr(), 0, 0, n, o.data_ptr(), None, streams[k % 6].cuda_stream)
         torch.cuda.synchronize()
     finally:
-        lib.pm_hip_debug_spill_cap(0)
+        m.set_option("spill_cap_chunks", 0)
     for o in outs:
         assert torch.equal(o, want)
 
@@ -1164,29 +1164,28 @@ def test_first_scan_device_inside_graph_capture(kind):
 
 
 def test_spill_cap_raised_after_prepare():
-    """A spill cap raised after the capture scratch was sized (timing
-    sweeps) clamps the captured launch's regions to the scratch instead of
-    failing it; the ids stay exact."""
+    """A spill cap raised after the capture scratch was sized (the
+    "spill_cap_chunks" option: 2 chunks when prepare_capture sized the
+    scratch, the default 16 at the captured launch) clamps the captured
+    launch's regions to the scratch instead of failing it; the ids stay
+    exact."""
     import torch
     n = 128 << 20  # 32 chunks per wave: past the default 16-chunk regions
     dt = torch.from_numpy(np.concatenate([_tiled_ship(n), np.zeros(64, np.uint8)])).cuda()
     want = torch.empty(n, dtype=torch.int32, device="cuda")
     matcher("et", "ac").scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None,
                                     torch.cuda.current_stream().cuda_stream)
-    lib = pm.load()
     m = fresh_matcher("et", "rt")
+    m.set_option("spill_cap_chunks", 2)
     m.prepare_capture()
+    m.set_option("spill_cap_chunks", 0)
     s = torch.cuda.Stream()
     got = torch.zeros(n, dtype=torch.int32, device="cuda")
-    try:
-        lib.pm_hip_debug_spill_cap(64)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
-        g.replay()
-        torch.cuda.synchronize()
-    finally:
-        lib.pm_hip_debug_spill_cap(0)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
+    g.replay()
+    torch.cuda.synchronize()
     assert torch.equal(got, want)
 
 

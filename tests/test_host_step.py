@@ -34,7 +34,10 @@ def host_scan(img, text, dense_rows=0):
     return out[:len(text)]
 
 
-FORMS = [(pm.KIND_RT, 0), (pm.KIND_AC, 0), (pm.KIND_AC, 1)]
+# (kind, dense_rows): the RT walk, the DFA's sparse form, its dense rows, and
+# the fallback-linked form's host reference (pm_fl_host_step, the device
+# kernel's step)
+FORMS = [(pm.KIND_RT, 0), (pm.KIND_AC, 0), (pm.KIND_AC, 1), (pm.KIND_AC, 2)]
 
 
 @pytest.mark.parametrize("key", ["et", "snort", "merged"])
