@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Where a 100 KiB read_block_gid call's time goes (the
+reference's chunk, measure.c:77 STREAM_BUFFER_SIZE, one read_block per chunk
+at measure.c:284), each piece as its own synchronous round trip, wall
+microseconds per call (median of 300, snort, RT kind, ASCII):
+  round_trip_empty   a one-element device op + stream synchronize: launch
+                     and completion latency alone
+  kernel_hbm         scan_device on HBM-resident text into HBM ids + sync
+                     (the small kernel's own time plus that latency)
+  kernel_zc          the same reading pinned host text and writing pinned
+                     host ids (zero copy: what a small read_block launches)
+  graph_zc           kernel_zc captured once into a HIP graph, then replayed
+  write_zc_400k      a device copy of 400 KB into pinned host memory + sync
+                     (the link's share: the ids a call brings back)
+  read_block_gid     the whole call (staging, launch, wait, result copy)
+  host_copy_400k     memcpy of 400 KB pinned -> pageable on the host
+Prints one JSON object."""
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import patternmatching_amd as pm  # noqa: E402
+
+N = 100 << 10
+REPS = 300
+lib = pm.load()
+d = pm.Dictionary([os.path.join(REPO, "tests", "golden", "data", "snort.dict")])
+m = pm.HipMatcher("rt")
+m.add_dictionary(d)
+m.compile()
+text = pm.gen_stream(N + 4096, 1, 0)
+s = torch.cuda.Stream()
+sp = s.cuda_stream
+
+
+def timeit(fn, reps=REPS):
+    for _ in range(20):
+        fn()
+    t = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        t.append(time.perf_counter() - t0)
+    return round(statistics.median(t) * 1e6, 2)
+
+
+res = {"chunk_bytes": N, "reps": REPS}
+one = torch.zeros(1, device="cuda")
+
+
+def empty():
+    with torch.cuda.stream(s):
+        one.add_(1)
+    s.synchronize()
+
+
+res["round_trip_empty_us"] = timeit(empty)
+dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+dout = torch.empty(N, dtype=torch.int32, device="cuda")
+
+
+def kernel_hbm():
+    m.scan_device(dt.data_ptr(), 0, 4096, N, dout.data_ptr(), None, sp)
+    s.synchronize()
+
+
+res["kernel_hbm_us"] = timeit(kernel_hbm)
+ht = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).pin_memory()
+hout = torch.empty(N, dtype=torch.int32).pin_memory()
+
+
+def kernel_zc():
+    m.scan_device(ht.data_ptr(), 0, 4096, N, hout.data_ptr(), None, sp)
+    s.synchronize()
+
+
+res["kernel_zc_us"] = timeit(kernel_zc)
+ref = dout.cpu().numpy()
+assert np.array_equal(hout.numpy(), ref)
+m.prepare_capture()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g, stream=s):
+    m.scan_device(ht.data_ptr(), 0, 4096, N, hout.data_ptr(), None, sp)
+hout.zero_()
+
+
+def graph_zc():
+    g.replay()
+    s.synchronize()
+
+
+res["graph_zc_us"] = timeit(graph_zc)
+assert np.array_equal(hout.numpy(), ref)
+dsrc = torch.empty(N, dtype=torch.int32, device="cuda")
+
+
+def write_zc():
+    with torch.cuda.stream(s):
+        hout.copy_(dsrc, non_blocking=True)
+    s.synchronize()
+
+
+res["write_zc_400k_us"] = timeit(write_zc)
+gids = np.empty(N, np.uint32)
+part = np.ascontiguousarray(text[4096:4096 + N])
+
+
+def call():
+    lib.pm_hip_read_block_gid(m.obj, part.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), N,
+                              gids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+
+
+m.reset()
+res["read_block_gid_us"] = timeit(call)
+res["read_block_gid_GBps"] = round(N / res["read_block_gid_us"] / 1e3, 3)
+dst = np.empty(N, np.uint32)
+hn = hout.numpy()
+res["host_copy_400k_us"] = timeit(lambda: np.copyto(dst, hn))
+print(json.dumps(res))

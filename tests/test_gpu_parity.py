@@ -634,6 +634,64 @@ def test_full_size_merged_4gib_kernels_agree():
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("stream", ["lines", "ship"])
+def test_full_size_merged_deep_auto_oracle_windows(stream):
+    """The reference's published dictionary (snort + et merged, results.csv:
+    2-4) on deep input at 1 GiB through the auto kind -- the bench's
+    merged_lines_auto and merged_ship_auto legs, seed 1: once the pick holds
+    (the measured RT launch, then the DFA trials) the held kernel's ids equal
+    the RT kernel's at every position, its count is the nonzero ids', and
+    oracle windows (each with max_len-1 bytes of context) match at random
+    offsets, at the held DFA kernel's segment starts (4 KiB apart at this
+    size: warm-ups from the last synchronizing 3-gram) and at both ends."""
+    torch = _torch()
+    rt, au = matcher("merged", "rt"), matcher("merged", "auto")
+    n = 1 << 30
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    if stream == "lines":
+        au.gen_lines_device(dt.data_ptr(), n + 64, 1, s)
+    else:
+        dt.copy_(torch.from_numpy(np.tile(SHIP, (n + 64) // len(SHIP) + 1)[: n + 64]).cuda())
+    ref = torch.empty(n, dtype=torch.int32, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, ref.data_ptr(), None, s)
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    c = torch.zeros(1, dtype=torch.int64, device="cuda")
+    held = au.hold_choice(0)
+    for _ in range(12):  # the pick: launches synchronized one by one until it holds
+        if held != -1:
+            break
+        au.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), None, s)
+        torch.cuda.synchronize()
+        held = au.hold_choice(0)
+    held = au.hold_choice(2)
+    assert held in (1, 2, 3)
+    a.zero_()
+    au.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, ref), held
+    assert int(c.item()) == int((ref != 0).sum().item())
+    if stream == "lines":  # deep, no period: a DFA form holds
+        assert au.kernel_last == 2, held
+    del ref
+    o = oracle_for("merged")
+    W = o.max_len - 1
+    rng = np.random.default_rng(2)
+    windows = (rng.integers(W, n - 100000, size=4).tolist() + [k * 4096 - 96 for k in (1, 4097, 131073, 262000)]
+               + [0, n - 65536])
+    for off in windows:
+        lo = max(0, off - W)
+        o.reset()
+        seg = dt[lo:off + 65536].cpu().numpy()
+        exp = o.scan_codes(seg)[off - lo:]
+        got = au._codes[a[off:off + 65536].cpu().numpy().view(np.uint32)]
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (off, held, bad[:5])
+    del a, dt
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.slow
 @pytest.mark.parametrize("stream", ["bytes", "ship"])
 def test_full_size_binary_and_deep_streams_kernels_agree(stream):
     """1 GiB of uniform bytes (every byte value, snort's binary patterns) and
