@@ -120,9 +120,11 @@ int pm_hip_hold_choice(void* obj, int launches);
  * torch.cuda.graph): allocates the scratch captured launches of the rt / auto
  * kinds use (the reverse-trie kernel's spill regions, sized for a launch of
  * any length: 512 MiB on 256 CUs), since nothing may be allocated while a
- * stream captures.  Without it a captured scan_device returns -5 and
- * launches nothing.  Direct launches allocate their own scratch per stream
- * (pm_hip_scratch_bytes).  0 on success. */
+ * stream captures.  Without it a captured scan_device that would run the
+ * chunked reverse-trie kernel (more than 256 Ki positions, the "rt_small_max"
+ * option) returns -5 and launches nothing; smaller launches, and launches of
+ * an auto object holding a DFA form, need none.  Direct launches allocate
+ * their own scratch per stream (pm_hip_scratch_bytes).  0 on success. */
 int pm_hip_prepare_capture(void* obj);
 /* Device scratch the object holds beside its tables (pm_hip_table_bytes):
  * the capture scratch, the per-stream scratch of direct scan_device

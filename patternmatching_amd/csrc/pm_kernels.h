@@ -4,6 +4,10 @@
 #include <cstdint>
 
 constexpr size_t RT_SCRATCH_BYTES = 4096;
+// RT launches of at most this many positions take the one-thread-per-
+// position kernel, which needs no spill scratch (RtDev::small_max
+// overrides it per object: 0 = never).
+constexpr int64_t RT_SMALL_MAX = (int64_t)256 << 10;
 
 struct RtDev {
     const uint16_t* t12;   // 65536 + 256 u16; the first 64K staged into LDS per workgroup

@@ -2169,9 +2169,6 @@ static int64_t rt_blocks(int64_t n, int num_cu) {
     if (b > num_cu) b = num_cu;
     return b < 1 ? 1 : b;
 }
-// Launches of at most this many positions take rt_small_kernel (RtDev::
-// small_max overrides it per object: 0 = never).
-constexpr int64_t RT_SMALL_MAX = (int64_t)256 << 10;
 // Spill items per wave region: one per position of the wave's main-loop
 // chunks, capped at RT_SPILL_WAVE_CAP (the kernel resolves a full region
 // and goes on, rt_scan_kernel): 128 KiB per wave, 512 MiB for a 1 GiB launch

@@ -1055,8 +1055,13 @@ static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         e = hipStreamIsCapturing(s, &cs);
         StreamSpill* sp = e == hipSuccess && cs == hipStreamCaptureStatusNone ? stream_spill(o, s, n) : nullptr;
-        if (e == hipSuccess && cs != hipStreamCaptureStatusNone && !o->spill &&
-            (o->kind == KIND_RT || o->kind == KIND_AUTO)) {
+        // Only the chunked RT kernel uses the scratch: a captured launch the
+        // one-thread-per-position kernel takes (n <= the small-launch
+        // bound), or one of an auto object whose held choice is a DFA form,
+        // needs no prepare_capture.
+        const int64_t small_max = o->rt.small_max >= 0 ? o->rt.small_max : RT_SMALL_MAX;
+        const bool rt_next = o->kind == KIND_RT || (o->kind == KIND_AUTO && o->pick.chosen == CAND_RT);
+        if (e == hipSuccess && cs != hipStreamCaptureStatusNone && !o->spill && rt_next && n > small_max) {
             // nothing launched: the capture stays valid for the caller to end
             std::snprintf(g_err, sizeof(g_err),
                           "scan_device under stream capture needs pm_hip_prepare_capture(obj) first (the RT "

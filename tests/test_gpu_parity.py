@@ -1204,6 +1204,16 @@ def test_first_scan_device_inside_graph_capture(kind):
             with torch.cuda.graph(g, stream=s):
                 bare.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
+        # a launch the one-thread-per-position kernel takes (<= 256 Ki
+        # positions) needs no scratch, so no prepare_capture
+        small = 100 << 10
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2, stream=s):
+            bare.scan_device(dt.data_ptr(), 0, 0, small, got.data_ptr(), None, s.cuda_stream)
+        got.zero_()
+        g2.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(got[:small], want[:small])
     m = fresh_matcher("et", kind)
     m.prepare_capture()
     assert m.scratch_bytes >= (0 if kind == "ac" else 1 << 20)
