@@ -125,3 +125,45 @@ def test_stream_generator_matches_spec():
         raw = (sm((7 << 40) | (i >> 3)) >> (8 * (i & 7))) & 0xFF
         assert b[i] == raw
         assert a[i] == 0x20 + ((raw * 95) >> 8)
+
+
+class _Conf(ctypes.Structure):
+    """PmConf (include/pm_host.h)."""
+    _fields_ = [("dict_files", ctypes.c_void_p), ("n_dict_files", ctypes.c_size_t),
+                ("stream_files", ctypes.c_void_p), ("n_stream_files", ctypes.c_size_t),
+                ("output_file", ctypes.c_char_p), ("matches_file", ctypes.c_char_p), ("verbose", ctypes.c_int),
+                ("algo_mask", ctypes.c_int), ("chunk_bytes", ctypes.c_size_t), ("device", ctypes.c_int)]
+
+
+class _Stats(ctypes.Structure):
+    """PmInstanceStats (include/pm_host.h)."""
+    _fields_ = [("wall_seconds", ctypes.c_double), ("device_seconds", ctypes.c_double), ("bytes", ctypes.c_uint64),
+                ("nonnull", ctypes.c_uint64), ("total_mem", ctypes.c_size_t),
+                ("sr", ctypes.c_uint64 * 4), ("out_width", ctypes.c_int)]
+
+
+def test_csv_device_columns_empty_when_unmeasured(tmp_path):
+    """pm_write_stats (the CLI's CSV, measure.c:339-408 plus GPU columns):
+    an instance whose device time was measured gets its device seconds,
+    GB/s and roofline fraction; one whose launches were not timed (the
+    "host_events" option off: pm_hip_device_seconds returns -1) gets empty
+    device columns, not zeros."""
+    lib = pm.load()
+    out = tmp_path / "stats.csv"
+    conf = _Conf(output_file=str(out).encode(), algo_mask=0b11, device=0)
+    stats = (_Stats * 3)()
+    for k, dev in ((0, 0.5), (1, -1.0)):
+        stats[k].wall_seconds = 1.0
+        stats[k].device_seconds = dev
+        stats[k].bytes = 1 << 30
+        stats[k].sr[0] = 1 << 30  # success
+        stats[k].out_width = 4
+    assert lib.pm_write_stats(ctypes.byref(conf), stats) == 0
+    rows = [r.split(",") for r in out.read_text().strip().split("\n")]
+    head = rows[0]
+    i_t, i_g, i_f = head.index("Device Time (in secs)"), head.index("Device GB/s"), head.index("Device Roofline Fraction")
+    measured, unmeasured = rows[1], rows[2]
+    assert float(measured[i_t]) == 0.5 and abs(float(measured[i_g]) - (1 << 30) / 0.5 / 1e9) < 1e-3
+    assert abs(float(measured[i_f]) - (1 << 30) / 0.5 / 1e9 * 5 / 8000.0) < 1e-6
+    assert unmeasured[i_t] == unmeasured[i_g] == unmeasured[i_f] == ""
+    assert len(measured) == len(unmeasured) == len(head)
