@@ -545,12 +545,18 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
     auto R = [&](uint32_t v) { return rec + (size_t)(v - F) * 4; };  // {x, y, z, w} of record v
     for (uint32_t v = 0; v < S; ++v)
         if (d.sout[v] >= 65536) return false;
-    // rows by fallback use (the root first: the warm-ups start there)
+    // rows: the first PM_FL_LDS_ROWS in the trie's breadth-first order (the
+    // root and the shallowest states: the rows the kernel stages in LDS, as
+    // the 8-B form does -- most row steps are theirs), then the others by
+    // fallback use, so the word's 11-bit field names the most used ones
+    // (scripts/sdfa_spec_model.cpp BFS88: lines stream 0.697 -> 0.662
+    // global requests per step, random ASCII 0.729 -> 0.699)
     std::vector<uint64_t> use(F, 0);
     for (uint32_t v = F; v < S; ++v) use[R(v)[3]]++;
     std::vector<uint32_t> ord(F), nrow(F);
     for (uint32_t r = 0; r < F; ++r) ord[r] = r;
-    std::stable_sort(ord.begin() + 1, ord.end(), [&](uint32_t a, uint32_t b) { return use[a] > use[b]; });
+    const uint32_t keep = std::min(F, PM_FL_LDS_ROWS);
+    std::stable_sort(ord.begin() + keep, ord.end(), [&](uint32_t a, uint32_t b) { return use[a] > use[b]; });
     for (uint32_t k = 0; k < F; ++k) nrow[ord[k]] = k;
     // folded slotless records; granules of the others
     std::vector<uint8_t> fold(S, 0);

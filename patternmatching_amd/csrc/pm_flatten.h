@@ -172,9 +172,10 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
 // lanes in lock step nearly every wave step waits for some lane's pair.
 // Here the word that leads INTO a record names its fallback row, so the
 // block and the row word can be loaded together.
-//   Rows [0, F): renumbered by how many records fall back to them (the root
-//   stays 0), so the fallback rows records use most have the smallest ids
-//   (and the first ones are the rows the kernel stages in LDS).
+//   Rows [0, F): the first PM_FL_LDS_ROWS keep the trie's breadth-first
+//   order (the root and the shallowest states, staged in LDS by the
+//   kernel), the rest are renumbered by how many records fall back to
+//   them, so the fallback rows records use most have the smallest ids.
 //   Records: in the trie's order, at 8-B granules (state id = F + granule):
 //     word0 = out16 | c0 << 16 | c1 << 24   out16 = the record's OWN output
 //             (gid < 65536); c1 == c0 for one slot (a slotless record that
@@ -200,6 +201,7 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
 // False when it does not apply: 65,536 patterns or rows or more, or ids past
 // the 20-bit target field.
 constexpr uint32_t PM_FL_FB_INREC = 2047;
+constexpr uint32_t PM_FL_LDS_ROWS = 88;  // rows the kernel stages in LDS (dfa_fl_kernel<88>)
 struct FlImage {
     std::vector<uint32_t> block;     // F * 256 row words, then 2 words per granule
     std::vector<uint16_t> rowout16;  // output of each row (escapes)

@@ -1197,6 +1197,7 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
 constexpr uint32_t DFA_STATE_MASK = 0xFFFFFu;  // must match pm_flatten.h
 constexpr uint32_t DFA_ESC = 4095u;
 constexpr uint32_t PM_FL_INREC = 2047u;  // must match pm_flatten.h PM_FL_FB_INREC
+constexpr int FL_LDS_ROWS = 88;          // must match pm_flatten.h PM_FL_LDS_ROWS
 
 // The start of the last synchronizing 3-gram in [wlo, lo - 3], or wlo when
 // there is none (DfaDev::gram3: no pattern holds it, so the state after it is
@@ -1363,6 +1364,14 @@ __device__ __forceinline__ uint4 pick4(const uint4 (&R)[4], uint32_t k) {
 // (measured and removed: the fallback rows' words read non-temporally, so
 // row lines -- 64 B of which a step uses 4 -- would leave L2 to the
 // records: lines 5.46 -> 8.80 ms; profiles/r04/gid_order/stage16_nt_rows_ab.json)
+// Branch-free selects: (m & b) | (~m & a) is one v_bfi_b32.  (Written as
+// ternaries, the compiler turned a record's word picks into exec-mask
+// branches -- the first fallback-linked kernel had 2.2x the scalar and 1.5x
+// the vector instructions of the 8-B-unit kernel per step and measured
+// 13-30% slower.)
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (m & b) | (~m & a); }
+__device__ __forceinline__ uint32_t bmask(bool c) { return 0u - (uint32_t)c; }
+
 template <int KR, int RB = 16, int BU = 8>
 __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ base, uint32_t F,
                                                   const uint32_t* __restrict__ s_rows, uint32_t s, uint32_t c,
@@ -1370,37 +1379,64 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
     static_assert(BU == 8 || (BU == 4 && RB == 8), "4-unit blocks are 8-B units");
     const bool isrow = s < F;
     const uint32_t rec = s - F, b = rec >> (RB == 8 ? (BU == 8 ? 3 : 2) : 2);
+    if (RB == 8) {
+        // one guarded site per load, selects (v_bfi) elsewhere
+        const bool lrow = KR && isrow && s < (uint32_t)KR;
+        uint32_t rv = 0;
+        if (isrow && !lrow) rv = *reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
+        if (!isrow && b != cb) {
+            const uint4* p = reinterpret_cast<const uint4*>(base + F * 1024u + b * (BU == 8 ? 64u : 32u));
+            R[0] = p[0];
+            R[1] = p[1];
+            if (BU == 8) {
+                R[2] = p[2];
+                R[3] = p[3];
+            }
+            cb = b;
+        }
+        const uint32_t lw = KR ? s_rows[(bmask(lrow) & s) * 256u + c] : 0u;
+        // unit e = {y, x} and the next unit {z, w2} (a two-unit record never
+        // straddles an aligned 32-B block)
+        const uint32_t e = rec & (BU - 1u);
+        const uint32_t m1 = bmask(e & 1u), m2 = bmask(e & 2u);
+        uint4 A = R[0], B = R[1];
+        if (BU == 8) {
+            const uint32_t m4 = bmask(e & 4u);
+            A = make_uint4(bsel(m4, R[0].x, R[2].x), bsel(m4, R[0].y, R[2].y), bsel(m4, R[0].z, R[2].z),
+                           bsel(m4, R[0].w, R[2].w));
+            B = make_uint4(bsel(m4, R[1].x, R[3].x), bsel(m4, R[1].y, R[3].y), bsel(m4, R[1].z, R[3].z),
+                           bsel(m4, R[1].w, R[3].w));
+        }
+        const uint32_t y = bsel(m2, bsel(m1, A.x, A.z), bsel(m1, B.x, B.z));
+        const uint32_t x = bsel(m2, bsel(m1, A.y, A.w), bsel(m1, B.y, B.w));
+        const uint32_t z = bsel(m2, bsel(m1, A.z, B.x), B.z);
+        const uint32_t w2 = bsel(m2, bsel(m1, A.w, B.y), B.w);
+        const uint32_t key = c | 0x100u;
+        const bool two = x >> 31;
+        const bool h0 = (x & 0x1FFu) == key, h1 = two && ((x >> 16) & 0x1FFu) == key;
+        const uint32_t w = bsel(bmask(two), (x >> 9) & 0x3FFFFFu, w2);  // the fallback row
+        uint32_t mv = 0;
+        if (!isrow && !h0 && !h1) {
+            if (KR && w < (uint32_t)KR) mv = s_rows[w * 256u + c];
+            else mv = *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
+        }
+        const uint32_t rrec = bsel(bmask(h0), bsel(bmask(h1), mv, z), y);
+        return bsel(bmask(isrow), rrec, bsel(bmask(lrow), rv, lw));
+    }
     uint32_t rv = 0;
     if (isrow) {
         if (KR && s < (uint32_t)KR) rv = s_rows[s * 256u + c];
         else rv = *reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
     } else if (b != cb) {
-        const uint4* p = reinterpret_cast<const uint4*>(base + F * 1024u + b * (BU == 8 ? 64u : 32u));
+        const uint4* p = reinterpret_cast<const uint4*>(base + F * 1024u + b * 64u);
         R[0] = p[0];
         R[1] = p[1];
-        if (BU == 8) {
-            R[2] = p[2];
-            R[3] = p[3];
-        }
+        R[2] = p[2];
+        R[3] = p[3];
         cb = b;
     }
     if (isrow) return rv;
     const uint32_t key = c | 0x100u;
-    if (RB == 8) {
-        const uint32_t e = rec & (BU - 1u);
-        const uint4 q = BU == 8 ? pick4(R, e >> 1) : ((e & 2u) ? R[1] : R[0]);
-        const uint4 q2 = BU == 8 ? pick4(R, ((e >> 1) + 1u) & 3u) : ((e & 2u) ? R[0] : R[1]);
-        const uint32_t y = (e & 1u) ? q.z : q.x, x = (e & 1u) ? q.w : q.y;
-        if ((x & 0x1FFu) == key) return y;
-        uint32_t w = (x >> 9) & 0x3FFFFFu;
-        if (x >> 31) {
-            const uint32_t z = (e & 1u) ? q2.x : q.z;
-            if (((x >> 16) & 0x1FFu) == key) return z;
-            w = (e & 1u) ? q2.y : q.w;
-        }
-        if (KR && w < (uint32_t)KR) return s_rows[w * 256u + c];
-        return *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
-    }
     const uint4 q = pick4(R, rec & 3u);
     if ((q.x & 0x1FFu) == key) return q.y;
     if (((q.x >> 16) & 0x1FFu) == key) return q.z;
@@ -1409,8 +1445,9 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
     return *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
 }
 
+// (two 512-lane workgroups per CU: 4 waves per SIMD, so at most 128 VGPRs)
 template <int OUTW, int BLK, int KR, int CH = 1, int RB = 16, int TB = 1>
-__global__ __launch_bounds__(DFA_LDS_THREADS) void dfa_sparse_lds_kernel(
+__global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void dfa_sparse_lds_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
     const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
@@ -1829,42 +1866,47 @@ __global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
 #ifndef PM_FL_SPEC
 #define PM_FL_SPEC 1
 #endif
+
 template <int KR>
 __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, uint32_t F,
                                             const uint32_t* __restrict__ s_rows, uint32_t w, uint32_t c,
                                             uint32_t& cb, tu32x4& R0, tu32x4& R1, uint32_t& own) {
     const uint32_t s = w & DFA_STATE_MASK;
     const bool isrow = s < F;
-    const uint32_t g = s - F, blk = g >> 2, e = g & 3u;
+    const uint32_t g = s - F, blk = g >> 2;
     const uint32_t fb = (w >> 20) & PM_FL_INREC;
-    uint32_t rw = 0, fw = 0;
-    bool pre = false;
-    if (isrow) {
-        if (KR && s < (uint32_t)KR) rw = s_rows[s * 256u + c];
-        else rw = *reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
-    } else if (blk != cb) {
+    const bool newblk = !isrow && blk != cb;
+    const bool pre = newblk && (PM_FL_SPEC == 2 || (PM_FL_SPEC == 1 && (w >> 31))) && fb != PM_FL_INREC &&
+                     fb >= (uint32_t)KR;
+    const bool lrow = isrow && s < (uint32_t)KR;
+    // the global word: a row state's word, or a new miss-prone record's
+    // fallback word loaded with its block
+    uint32_t x = 0;
+    if ((isrow && !lrow) || pre) x = *reinterpret_cast<const uint32_t*>(base + bsel(bmask(isrow), fb, s) * 1024u + c * 4u);
+    if (newblk) {
         const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * 32u);
         R0 = p[0];
         R1 = p[1];
         cb = blk;
-        // a miss-prone record entered in a new block: its fallback row's
-        // word in the same round of loads (LDS rows need no head start)
-        pre = (PM_FL_SPEC == 2 || (PM_FL_SPEC == 1 && (w >> 31))) && fb != PM_FL_INREC && fb >= (uint32_t)KR;
-        if (pre) fw = *reinterpret_cast<const uint32_t*>(base + fb * 1024u + c * 4u);
     }
-    if (isrow) return rw;
+    const uint32_t lw = s_rows[(bmask(lrow) & s) * 256u + c];  // (row 0 for the other lanes: no branch)
     // words 2e .. 2e + 3 of the block (a 16-B record never sits at e = 3)
-    const uint32_t w0 = (e & 2u) ? ((e & 1u) ? R1.z : R1.x) : ((e & 1u) ? R0.z : R0.x);
-    const uint32_t w1 = (e & 2u) ? ((e & 1u) ? R1.w : R1.y) : ((e & 1u) ? R0.w : R0.y);
+    const uint32_t m1 = bmask(g & 1u), m2 = bmask(g & 2u);
+    const uint32_t w0 = bsel(m2, bsel(m1, R0.x, R0.z), bsel(m1, R1.x, R1.z));
+    const uint32_t w1 = bsel(m2, bsel(m1, R0.y, R0.w), bsel(m1, R1.y, R1.w));
+    const uint32_t w2 = bsel(m2, bsel(m1, R0.z, R1.x), R1.z);
+    const uint32_t w3 = bsel(m2, bsel(m1, R0.w, R1.y), R1.w);
     own = w0 & 0xFFFFu;
-    if (c == ((w0 >> 16) & 0xFFu)) return w1;
-    const uint32_t w2 = (e & 2u) ? R1.z : ((e & 1u) ? R1.x : R0.z);
-    if (c == (w0 >> 24)) return w2;
-    if (pre) return fw;
-    const uint32_t w3 = (e & 2u) ? R1.w : ((e & 1u) ? R1.y : R0.w);
-    const uint32_t row = fb == PM_FL_INREC ? w3 : fb;
-    if (KR && row < (uint32_t)KR) return s_rows[row * 256u + c];
-    return *reinterpret_cast<const uint32_t*>(base + row * 1024u + c * 4u);
+    const bool h0 = c == ((w0 >> 16) & 0xFFu), h1 = c == (w0 >> 24);
+    const uint32_t row = bsel(bmask(fb == PM_FL_INREC), fb, w3);
+    // a record's miss without the early word: its fallback row, now
+    uint32_t y = 0;
+    if (!isrow && !h0 && !h1 && !pre) {
+        if (KR && row < (uint32_t)KR) y = s_rows[row * 256u + c];
+        else y = *reinterpret_cast<const uint32_t*>(base + row * 1024u + c * 4u);
+    }
+    const uint32_t rec = bsel(bmask(h0), bsel(bmask(h1), bsel(bmask(pre), y, x), w2), w1);
+    return bsel(bmask(isrow), rec, bsel(bmask(lrow), x, lw));
 }
 
 // The output of the position that produced w: a record's own out16 (its
@@ -2341,7 +2383,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         const dim3 gs((unsigned)wg), bs(wgt);
         switch (sk) {
             case PM_SK_FL:
-                hipLaunchKernelGGL((dfa_fl_kernel<88, true>), gs, bs, 0, s, text, stream_start, pos0, n,
+                hipLaunchKernelGGL((dfa_fl_kernel<FL_LDS_ROWS, true>), gs, bs, 0, s, text, stream_start, pos0, n,
                                    reinterpret_cast<uint32_t*>(out), count, t.flbase, t.flF, t.flrowout16, t.warm, seg,
                                    g3);
                 break;

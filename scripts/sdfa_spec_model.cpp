@@ -56,6 +56,11 @@ int main(int argc, char** argv) {
     const uint32_t* REC = B + (size_t)F * 256;
     const int KR = envi("KR", 88), WAVES = envi("WAVES", 64), SEG = envi("SEG", 4096), SPECALL = envi("SPECALL", 0);
     const uint32_t WLIM = envi("WLIM", 2047);  // fallback rows the word can name (11 bits + a speculate bit)
+    // BFS88 = 1: the first KR rows keep the trie's breadth-first order (the
+    // shallowest states, as the 8-B form stages them), the rest by fallback
+    // use; SPEC: 0 none, 1 non-chain records, 2 every new block; ASCII = 1:
+    // the random ASCII stream instead of the lines stream
+    const int BFS88 = envi("BFS88", 0), SPEC = envi("SPEC", 1), ASCII = envi("ASCII", 0);
     // cur: 8-B unit offsets, 32-B blocks
     std::vector<uint32_t> cur_blk(S, 0), new_blk(S, 0);
     {
@@ -74,6 +79,9 @@ int main(int argc, char** argv) {
     use[0] = ~0ull;  // the root stays row 0 (the warm-up's start)
     std::vector<uint32_t> ord(F), rank(F);
     for (uint32_t r = 0; r < F; ++r) ord[r] = r;
+    if (BFS88) {
+        for (uint32_t r = 0; r < F && r < (uint32_t)KR; ++r) use[r] = ~0ull - r;  // keep 0..KR-1 first, in order
+    }
     std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return use[a] > use[b]; });
     for (uint32_t k = 0; k < F; ++k) rank[ord[k]] = k;
     std::vector<uint8_t> fold(S, 0), chain(S, 0);
@@ -113,7 +121,7 @@ int main(int argc, char** argv) {
             for (uint64_t p = lo; p < lo + 512 + SEG; ++p) {
                 if (p % PM_LINES_BLOCK == 0 || p == lo)
                     pm_lines_block(blk.data(), PM_LINES_BLOCK, p / PM_LINES_BLOCK, P.data(), O.data(), pats.size(), 1);
-                txt[L].push_back(blk[p % PM_LINES_BLOCK]);
+                txt[L].push_back(ASCII ? pm_stream_byte(p, 1, 0) : blk[p % PM_LINES_BLOCK]);
             }
         }
     }
@@ -143,7 +151,7 @@ int main(int argc, char** argv) {
                         const bool hit0 = (r[0] & 0x1FF) == key, hit1 = ((r[0] >> 16) & 0x1FF) == key;
                         const uint32_t wr = r[3];
                         const bool wlds = design ? rank[wr] < (uint32_t)KR : wr < (uint32_t)KR;
-                        const bool spec = design && (SPECALL || !chain[st]) && rank[wr] < WLIM && !wlds;
+                        const bool spec = design && SPEC && (SPECALL || SPEC == 2 || !chain[st]) && rank[wr] < WLIM && !wlds;
                         req += cnt && nb;
                         if (hit0 || hit1) {
                             v = hit0 ? r[1] : r[2];

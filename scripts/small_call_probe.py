@@ -120,7 +120,7 @@ def call():
 m.reset()
 res["read_block_gid_us"] = timeit(call)
 res["read_block_gid_GBps"] = round(N / res["read_block_gid_us"] / 1e3, 3)
-dst = np.empty(N, np.uint32)
+dst = np.empty(N, np.int32)
 hn = hout.numpy()
 res["host_copy_400k_us"] = timeit(lambda: np.copyto(dst, hn))
 print(json.dumps(res))
