@@ -548,7 +548,7 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
     // rows: the first PM_FL_LDS_ROWS in the trie's breadth-first order (the
     // root and the shallowest states: the rows the kernel stages in LDS, as
     // the 8-B form does -- most row steps are theirs), then the others by
-    // fallback use, so the word's 11-bit field names the most used ones
+    // fallback use, so the word's 12-bit field names the most used ones
     // (scripts/sdfa_spec_model.cpp BFS88: lines stream 0.697 -> 0.662
     // global requests per step, random ASCII 0.729 -> 0.699)
     std::vector<uint64_t> use(F, 0);
@@ -571,7 +571,7 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
             continue;
         }
         const bool wide = s1 || nrow[r[3]] >= PM_FL_FB_INREC;
-        if (wide && (u & 3) == 3) ++u;  // 16 B inside one aligned 32-B block
+        if (wide && (u & 1)) ++u;  // 16 B at a 16-B boundary (the kernel's blocks: 16 or 32 B)
         gid[v] = (uint32_t)u;
         u += wide ? 2 : 1;
         if (F + u > PM_DFA_STATE_MASK + 1) return false;
@@ -583,10 +583,7 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
         if (t < F) return nrow[t] | std::min(d.sout[t], PM_DFA_ESC) << 20;
         const uint32_t* r = R(t);
         if (fold[t]) return nrow[r[3]] | d.sout[t] << 20;
-        const bool s0 = r[0] & 0x100u, s1 = r[0] & 0x1000000u;
-        const bool chain = (s0 && (r[1] & PM_DFA_STATE_MASK) == t + 1) || (s1 && (r[2] & PM_DFA_STATE_MASK) == t + 1);
-        const uint32_t fb = std::min(nrow[r[3]], PM_FL_FB_INREC);
-        return (F + gid[t]) | ((chain ? 0u : 1u) << 11 | fb) << 20;
+        return (F + gid[t]) | std::min(nrow[r[3]], PM_FL_FB_INREC) << 20;
     };
     fl.block.assign((size_t)F * 256 + 2 * (size_t)u, 0);
     fl.rowout16.assign(F, 0);
@@ -637,7 +634,7 @@ uint32_t pm_fl_host_step(const FlImage& fl, uint32_t w, uint8_t c, uint32_t* out
     const uint32_t* U = fl.block.data() + (size_t)fl.F * 256 + 2 * (size_t)(s - fl.F);
     if (c == ((U[0] >> 16) & 0xFFu)) return U[1];
     if (c == U[0] >> 24) return U[2];
-    const uint32_t fb = (w >> 20) & PM_FL_FB_INREC;
+    const uint32_t fb = w >> 20;
     const uint32_t row = fb == PM_FL_FB_INREC ? U[3] : fb;
     return fl.block[(size_t)row * 256 + c];
 }

@@ -170,8 +170,8 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
 // record in a block it does not hold waits for the block and then, at a
 // slot miss, for the fallback row's word: two dependent loads, and with 64
 // lanes in lock step nearly every wave step waits for some lane's pair.
-// Here the word that leads INTO a record names its fallback row, so the
-// block and the row word can be loaded together.
+// Here the word that leads INTO a record names its fallback row, so a
+// record needs no room for it and carries its own output instead.
 //   Rows [0, F): the first PM_FL_LDS_ROWS keep the trie's breadth-first
 //   order (the root and the shallowest states, staged in LDS by the
 //   kernel), the rest are renumbered by how many records fall back to
@@ -184,15 +184,12 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
 //     word1 = the word on c0
 //     16-B records (two slots, or a fallback outside the word's range):
 //     word2 = the word on c1 (word1 again for one slot), word3 = the
-//             fallback row; never straddling an aligned 32-B block.
+//             fallback row; 16-B aligned.
 //   A word (in rows and records): target | f << 20 with
 //     target a row: f = min(output of the target, PM_DFA_ESC) (escapes:
 //       FlImage::rowout16[target]);
-//     target a record: f = spec << 11 | fb, fb = its fallback row when that
-//       is < PM_FL_FB_INREC, else PM_FL_FB_INREC (the fallback is word3);
-//       spec = 1 when the record is not a chain interior (no slot to the
-//       next record), i.e. when a miss is likely: the kernel then loads the
-//       fallback row's word together with the record's block.
+//     target a record: f = its fallback row when that is below
+//       PM_FL_FB_INREC, else PM_FL_FB_INREC (the fallback is word3).
 //   The output of a position whose state is a record is that record's out16
 //   (read with the record at the next step); of a row state, the word's f.
 //   A slotless record whose output has an inline code is folded: every word
@@ -200,7 +197,7 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
 //   the same transitions, the same outputs.
 // False when it does not apply: 65,536 patterns or rows or more, or ids past
 // the 20-bit target field.
-constexpr uint32_t PM_FL_FB_INREC = 2047;
+constexpr uint32_t PM_FL_FB_INREC = 4095;  // the 12-bit field's top value
 constexpr uint32_t PM_FL_LDS_ROWS = 88;  // rows the kernel stages in LDS (dfa_fl_kernel<88>)
 struct FlImage {
     std::vector<uint32_t> block;     // F * 256 row words, then 2 words per granule

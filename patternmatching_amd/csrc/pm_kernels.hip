@@ -1196,7 +1196,7 @@ __global__ __launch_bounds__(DFA_THREADS) void dfa_scan_kernel(const uint8_t* __
 // per lane).  Escapes are looked up after each 16-step block, off the chain.
 constexpr uint32_t DFA_STATE_MASK = 0xFFFFFu;  // must match pm_flatten.h
 constexpr uint32_t DFA_ESC = 4095u;
-constexpr uint32_t PM_FL_INREC = 2047u;  // must match pm_flatten.h PM_FL_FB_INREC
+constexpr uint32_t PM_FL_INREC = 4095u;  // must match pm_flatten.h PM_FL_FB_INREC
 constexpr int FL_LDS_ROWS = 88;          // must match pm_flatten.h PM_FL_LDS_ROWS
 
 // The start of the last synchronizing 3-gram in [wlo, lo - 3], or wlo when
@@ -1383,7 +1383,7 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
         // one guarded site per load, selects (v_bfi) elsewhere
         const bool lrow = KR && isrow && s < (uint32_t)KR;
         uint32_t rv = 0;
-        if (isrow && !lrow) rv = *reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
+        if (isrow && !lrow) rv = *reinterpret_cast<const uint32_t*>(base + (s * 1024u + c * 4u));
         if (!isrow && b != cb) {
             const uint4* p = reinterpret_cast<const uint4*>(base + F * 1024u + b * (BU == 8 ? 64u : 32u));
             R[0] = p[0];
@@ -1418,7 +1418,7 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
         uint32_t mv = 0;
         if (!isrow && !h0 && !h1) {
             if (KR && w < (uint32_t)KR) mv = s_rows[w * 256u + c];
-            else mv = *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
+            else mv = *reinterpret_cast<const uint32_t*>(base + (w * 1024u + c * 4u));
         }
         const uint32_t rrec = bsel(bmask(h0), bsel(bmask(h1), mv, z), y);
         return bsel(bmask(isrow), rrec, bsel(bmask(lrow), rv, lw));
@@ -1426,7 +1426,7 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
     uint32_t rv = 0;
     if (isrow) {
         if (KR && s < (uint32_t)KR) rv = s_rows[s * 256u + c];
-        else rv = *reinterpret_cast<const uint32_t*>(base + s * 1024u + c * 4u);
+        else rv = *reinterpret_cast<const uint32_t*>(base + (s * 1024u + c * 4u));
     } else if (b != cb) {
         const uint4* p = reinterpret_cast<const uint4*>(base + F * 1024u + b * 64u);
         R[0] = p[0];
@@ -1442,7 +1442,7 @@ __device__ __forceinline__ uint32_t sdfa_lds_step(const uint8_t* __restrict__ ba
     if (((q.x >> 16) & 0x1FFu) == key) return q.z;
     const uint32_t w = q.w;  // the fallback row
     if (KR && w < (uint32_t)KR) return s_rows[w * 256u + c];
-    return *reinterpret_cast<const uint32_t*>(base + w * 1024u + c * 4u);
+    return *reinterpret_cast<const uint32_t*>(base + (w * 1024u + c * 4u));
 }
 
 // (two 512-lane workgroups per CU: 4 waves per SIMD, so at most 128 VGPRs)
@@ -1844,28 +1844,37 @@ __global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
 }
 
 // ---- the fallback-linked (FL) form (pm_flatten.h, pm_pack_sparse_fl) -----
-// The wave model of the 8-B form (scripts/sdfa_spec_model.cpp, lines stream,
-// 64 lanes in lock step) puts its wave steps at 1.77 dependent load
-// latencies: 2.3% of lane steps enter a record in a block the lane does not
-// hold and then miss its slots (the fallback row's word waits for the
-// block), and with 64 lanes 77% of wave steps hold such a lane.  In the FL
-// form the word that leads into a record names its fallback row, so a lane
-// entering a miss-prone record (not a chain interior: the word's spec bit)
-// loads the block and the fallback row's word together -- 1.22 latencies
-// per wave step modelled -- and a record carries its own output, so only
-// row outputs past the inline code escape.
+// The 8-B form's record holds its fallback row, so it has no room for the
+// record's own output: record states whose output is past the inline code
+// escape (a second pass over LDS and the global out8 table).  In the FL form
+// the word that leads into a record names the record's fallback row (12
+// bits; the rare fallbacks past that sit in the record), so a record
+// carries its own 16-bit output and only row outputs past the code escape.
+// (This was first built to let a lane load the block and the fallback row's
+// word together -- the wave model, scripts/sdfa_spec_model.cpp, put that at
+// 1.77 -> 1.22 dependent latencies per wave step -- but measured, the extra
+// requests cost more than the latency saved on the lines stream: snort
+// 5.09 ms/GiB without, 5.42 for non-chain records, 6.22 for every new
+// block; profiles/r05/ab/fl_spec_ablation.jsonl.  The product does not
+// speculate; the ablation build AB_HIPFLAGS=-DPM_FL_SPEC=2, scripts/
+// build_ab.sh, loads the fallback word with every new record block.)
 //
 // One step from the word w that led to the lane's state (state w & MASK;
-// for a record, the fallback row in bits 20-30 and the spec bit 31) on byte
-// c: returns the next word.  For a record state, own = its out16: the
-// output of the position that produced w.
-// (Ablation builds, scripts/build_ab.sh with AB_HIPFLAGS=-DPM_FL_SPEC=n:
-// 0 = never load the fallback row's word early, 2 = at every new block a
-// record with a fallback in the word enters; 1, the product: only for
-// records not in a chain interior.)
+// for a record, the fallback row in bits 20-31) on byte c: returns the next
+// word.  For a record state, own = its out16: the output of the position
+// that produced w.
 #ifndef PM_FL_SPEC
-#define PM_FL_SPEC 1
+#define PM_FL_SPEC 0
 #endif
+static_assert(PM_FL_SPEC == 0 || PM_FL_SPEC == 2, "PM_FL_SPEC: 0 (product) or 2 (ablation)");
+
+// A lane holds the aligned block of records its state is in (16 or 32 B:
+// one or two 16-B loads; PM_FL_BLK, an ablation switch of build_ab.sh).
+#ifndef PM_FL_BLK
+#define PM_FL_BLK 16
+#endif
+static_assert(PM_FL_BLK == 16 || PM_FL_BLK == 32, "PM_FL_BLK: 16 or 32");
+constexpr uint32_t FL_BLK_SHIFT = PM_FL_BLK == 16 ? 1u : 2u;  // granules per block: 2 or 4
 
 template <int KR>
 __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, uint32_t F,
@@ -1873,37 +1882,46 @@ __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, ui
                                             uint32_t& cb, tu32x4& R0, tu32x4& R1, uint32_t& own) {
     const uint32_t s = w & DFA_STATE_MASK;
     const bool isrow = s < F;
-    const uint32_t g = s - F, blk = g >> 2;
-    const uint32_t fb = (w >> 20) & PM_FL_INREC;
+    const uint32_t g = s - F, blk = g >> FL_BLK_SHIFT;
+    const uint32_t fb = w >> 20;
     const bool newblk = !isrow && blk != cb;
-    const bool pre = newblk && (PM_FL_SPEC == 2 || (PM_FL_SPEC == 1 && (w >> 31))) && fb != PM_FL_INREC &&
-                     fb >= (uint32_t)KR;
+    const bool pre = PM_FL_SPEC == 2 && newblk && fb != PM_FL_INREC && fb >= (uint32_t)KR;
     const bool lrow = isrow && s < (uint32_t)KR;
-    // the global word: a row state's word, or a new miss-prone record's
-    // fallback word loaded with its block
+    // the global word: a row state's word (or, PM_FL_SPEC 2, a new
+    // record's fallback word loaded with its block)
     uint32_t x = 0;
-    if ((isrow && !lrow) || pre) x = *reinterpret_cast<const uint32_t*>(base + bsel(bmask(isrow), fb, s) * 1024u + c * 4u);
+    if ((isrow && !lrow) || pre) x = *reinterpret_cast<const uint32_t*>(base + (bsel(bmask(isrow), fb, s) * 1024u + c * 4u));
     if (newblk) {
-        const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * 32u);
+        const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * (uint32_t)PM_FL_BLK);
         R0 = p[0];
-        R1 = p[1];
+        if (PM_FL_BLK == 32) R1 = p[1];
         cb = blk;
     }
     const uint32_t lw = s_rows[(bmask(lrow) & s) * 256u + c];  // (row 0 for the other lanes: no branch)
-    // words 2e .. 2e + 3 of the block (a 16-B record never sits at e = 3)
-    const uint32_t m1 = bmask(g & 1u), m2 = bmask(g & 2u);
-    const uint32_t w0 = bsel(m2, bsel(m1, R0.x, R0.z), bsel(m1, R1.x, R1.z));
-    const uint32_t w1 = bsel(m2, bsel(m1, R0.y, R0.w), bsel(m1, R1.y, R1.w));
-    const uint32_t w2 = bsel(m2, bsel(m1, R0.z, R1.x), R1.z);
-    const uint32_t w3 = bsel(m2, bsel(m1, R0.w, R1.y), R1.w);
+    // words 2e .. 2e + 3 of the block, e the granule in it (a 16-B record
+    // starts at an even granule)
+    const uint32_t m1 = bmask(g & 1u);
+    uint32_t w0, w1, w2, w3;
+    if (PM_FL_BLK == 16) {
+        w0 = bsel(m1, R0.x, R0.z);
+        w1 = bsel(m1, R0.y, R0.w);
+        w2 = R0.z;
+        w3 = R0.w;
+    } else {
+        const uint32_t m2 = bmask(g & 2u);
+        w0 = bsel(m2, bsel(m1, R0.x, R0.z), bsel(m1, R1.x, R1.z));
+        w1 = bsel(m2, bsel(m1, R0.y, R0.w), bsel(m1, R1.y, R1.w));
+        w2 = bsel(m2, R0.z, R1.z);
+        w3 = bsel(m2, R0.w, R1.w);
+    }
     own = w0 & 0xFFFFu;
     const bool h0 = c == ((w0 >> 16) & 0xFFu), h1 = c == (w0 >> 24);
     const uint32_t row = bsel(bmask(fb == PM_FL_INREC), fb, w3);
-    // a record's miss without the early word: its fallback row, now
+    // a record's miss: its fallback row's word
     uint32_t y = 0;
     if (!isrow && !h0 && !h1 && !pre) {
         if (KR && row < (uint32_t)KR) y = s_rows[row * 256u + c];
-        else y = *reinterpret_cast<const uint32_t*>(base + row * 1024u + c * 4u);
+        else y = *reinterpret_cast<const uint32_t*>(base + (row * 1024u + c * 4u));
     }
     const uint32_t rec = bsel(bmask(h0), bsel(bmask(h1), bsel(bmask(pre), y, x), w2), w1);
     return bsel(bmask(isrow), rec, bsel(bmask(lrow), x, lw));
@@ -1921,21 +1939,20 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
         esc = (w >> 20) == DFA_ESC;
         return w >> 20;
     }
-    const uint32_t g = s - F, blk = g >> 2, e = g & 3u;
+    const uint32_t g = s - F, blk = g >> FL_BLK_SHIFT;
     if (blk != cb) {
-        const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * 32u);
+        const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * (uint32_t)PM_FL_BLK);
         R0 = p[0];
-        R1 = p[1];
+        if (PM_FL_BLK == 32) R1 = p[1];
         cb = blk;
     }
-    const uint32_t w0 = (e & 2u) ? ((e & 1u) ? R1.z : R1.x) : ((e & 1u) ? R0.z : R0.x);
+    const uint32_t w0 = (PM_FL_BLK == 32 && (g & 2u)) ? ((g & 1u) ? R1.z : R1.x) : ((g & 1u) ? R0.z : R0.x);
     return w0 & 0xFFFFu;
 }
 
 // The FL form's scan: the staged-id structure of dfa_sparse_stage16_kernel
 // (u16 staging rows, escapes in rounds, whole-line non-temporal stores;
-// 1,024-lane workgroups, KR rows in LDS -- here the KR rows records fall
-// back to most), the FL step, and outputs one step late: a step writes the
+// 1,024-lane workgroups, the KR shallowest rows in LDS), the FL step, and outputs one step late: a step writes the
 // output of the position before it (the state it starts from holds it).
 template <int KR, bool NT = true>
 __global__ __launch_bounds__(1024) void dfa_fl_kernel(

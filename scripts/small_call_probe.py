@@ -12,7 +12,10 @@ microseconds per call (median of 300, snort, RT kind, ASCII):
   graph_zc           kernel_zc captured once into a HIP graph, then replayed
   write_zc_400k      a device copy of 400 KB into pinned host memory + sync
                      (the link's share: the ids a call brings back)
-  read_block_gid     the whole call (staging, launch, wait, result copy)
+  read_block_gid     the whole call (staging, launch, wait, result copy),
+                     its launch replayed from a captured HIP graph (the
+                     "host_graph" option, default on); _nograph: option off
+  read_block_ids     the same for pattern ids (read_block; ac kind too)
   host_copy_400k     memcpy of 400 KB pinned -> pageable on the host
 Prints one JSON object."""
 import ctypes
@@ -117,9 +120,28 @@ def call():
                               gids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
 
 
-m.reset()
-res["read_block_gid_us"] = timeit(call)
-res["read_block_gid_GBps"] = round(N / res["read_block_gid_us"] / 1e3, 3)
+ids = np.empty(N, np.uint64)
+
+
+def call_ids(mm):
+    return lambda: lib.pm_hip_read_block(mm.obj, part.ctypes.data_as(ctypes.c_char_p), N,
+                                         ids.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p)))
+
+
+ac = pm.HipMatcher("ac")
+ac.add_dictionary(d)
+ac.compile()
+for g, tag in ((1, ""), (0, "_nograph")):
+    for mm, kname in ((m, ""), (ac, "_ac")):
+        assert mm.set_option("host_graph", g) == 0
+        mm.reset()
+        fn = call if mm is m else (lambda: lib.pm_hip_read_block_gid(
+            ac.obj, part.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), N,
+            gids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+        res[f"read_block_gid{kname}{tag}_us"] = timeit(fn)
+        mm.reset()
+        res[f"read_block_ids{kname}{tag}_us"] = timeit(call_ids(mm))
+    res[f"read_block_gid{tag}_GBps"] = round(N / res[f"read_block_gid{tag}_us"] / 1e3, 3)
 dst = np.empty(N, np.int32)
 hn = hout.numpy()
 res["host_copy_400k_us"] = timeit(lambda: np.copyto(dst, hn))

@@ -457,6 +457,48 @@ def test_small_gid_calls_u16_and_u32(kind, key):
         m.free()
 
 
+@pytest.mark.parametrize("kind", KINDS)
+def test_small_calls_graph_replay(kind):
+    """The "host_graph" option (csrc/pm_plugin.hip launch_small): a small
+    read_block launch that repeats the previous call's (kernel, offsets,
+    size, width) is captured into a HIP graph and replayed after that.
+    Repeated, changing and returning chunk sizes -- ragged ends, a 1-byte
+    call, 255 Ki calls -- give the ids of one large call with graphs on and
+    off, for gids and pattern ids, and an option change between calls (which
+    drops the captured launches) changes nothing either."""
+    m = matcher("snort", kind)
+    sizes = [100 << 10] * 6 + [37 << 10] * 3 + [100 << 10] * 3 + [1, 1, 255 << 10, 255 << 10, 5000]
+    text = np.tile(SHIP, 1 + sum(sizes) // len(SHIP))[:sum(sizes)]
+    offs = np.cumsum([0] + sizes)
+    m.reset()
+    whole = m.read_block_gids(text)
+    m.reset()
+    whole_ids = m.read_block_id_array(text)
+    try:
+        for g in (1, 0, 1):
+            assert m.set_option("host_graph", g) == 0
+            m.reset()
+            parts = [m.read_block_gids(text[a:b]) for a, b in zip(offs[:-1], offs[1:])]
+            assert np.array_equal(np.concatenate(parts), whole), g
+            m.reset()
+            ids = [m.read_block_id_array(text[a:b]) for a, b in zip(offs[:-1], offs[1:])]
+            assert np.array_equal(np.concatenate(ids), whole_ids), g
+        # an option between calls: the next launches are the new option's
+        m.reset()
+        parts = [m.read_block_gids(text[a:b]) for a, b in zip(offs[:7], offs[1:8])]
+        if kind == "rt":
+            assert m.set_option("rt_small_max", 0) == 0  # the chunked RT kernel from here on
+        else:
+            assert m.set_option("dfa_form", 2) == 0 and m.set_option("sparse_kernel", 4) == 0
+        parts += [m.read_block_gids(text[a:b]) for a, b in zip(offs[7:-1], offs[8:])]
+        assert np.array_equal(np.concatenate(parts), whole)
+        if kind == "ac":
+            assert m.sparse_kernel_last == 4
+    finally:
+        for k, v in (("host_graph", -1), ("rt_small_max", -1), ("dfa_form", 0), ("sparse_kernel", 0)):
+            m.set_option(k, v)
+
+
 def _score_host(algo, real, parent, depth):
     """measure_success_rate (Core/src/measure.c:174-190) + all-matches, numpy."""
     algo = algo.astype(np.int64)
