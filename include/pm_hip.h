@@ -211,13 +211,12 @@ int pm_hip_set_device(int device);
  *                     0 = never)
  *   "spill_cap_chunks" the reverse-trie spill region per wave, 1,024-position
  *                     chunks (1..16; 0 = default 16)
- *   "host_spin" / "host_gid16" / "host_events" / "host_pool" / "host_graph"
+ *   "host_spin" / "host_gid16" / "host_events" / "host_pool"
  *                     read_block's host path (-1 = the environment's
  *                     default, 0 / 1; csrc/pm_plugin.hip HostOpts).
- *                     host_graph (default on): a small call's launch that
- *                     repeats the previous call's is replayed from a
- *                     captured HIP graph.  Setting any option drops the
- *                     captured launches. */
+ *                     host_events (default off): small read_block calls
+ *                     (<= 256 Ki positions) record timing events for
+ *                     pm_hip_device_seconds; the CLI turns it on */
 int pm_hip_set_option(void* obj, const char* name, int64_t value);
 /* The reverse-trie kernel's streaming floor on this GPU: the same chunk
  * loop's loads and stores with no lookups (its d_out values are not match

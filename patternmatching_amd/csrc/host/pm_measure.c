@@ -181,6 +181,8 @@ int pm_measure_all(PmConf* conf, PmDict* dict, PmInstanceStats* stats) {
         if (!(conf->algo_mask & (1 << a))) continue;
         if (first_algo < 0) first_algo = a;
         inst[a].obj = pm_mps_table[a].create();
+        /* the device-time columns: time every read_block launch, small ones too */
+        (void)pm_hip_set_option(inst[a].obj, "host_events", 1);
         pm_dict_feed(dict, &inst[a], feed_cb);
         pm_mps_table[a].compile(inst[a].obj);
     }
@@ -237,8 +239,8 @@ int pm_measure_all(PmConf* conf, PmDict* dict, PmInstanceStats* stats) {
             }
             close(fd);
             {
-                /* < 0: some launches were not timed (pm_hip_set_option
-                 * "host_events" 0) -- the device columns are then unmeasured */
+                /* < 0: some launches were not timed ("host_events" off) --
+                 * the device columns are then unmeasured */
                 const double ds = pm_hip_device_seconds(inst[a].obj);
                 if (ds < 0 || st->device_seconds < 0) st->device_seconds = -1.0;
                 else st->device_seconds += ds;

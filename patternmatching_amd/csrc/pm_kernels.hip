@@ -1198,6 +1198,9 @@ constexpr uint32_t DFA_STATE_MASK = 0xFFFFFu;  // must match pm_flatten.h
 constexpr uint32_t DFA_ESC = 4095u;
 constexpr uint32_t PM_FL_INREC = 4095u;  // must match pm_flatten.h PM_FL_FB_INREC
 constexpr int FL_LDS_ROWS = 88;          // must match pm_flatten.h PM_FL_LDS_ROWS
+// The count-only FL kernel has no staging rows: 156 rows fill the LDS (the
+// 88 shallowest, then the fallbacks records use most: pm_pack_sparse_fl's order).
+constexpr int FL_COUNT_LDS_ROWS = 156;
 
 // The start of the last synchronizing 3-gram in [wlo, lo - 3], or wlo when
 // there is none (DfaDev::gram3: no pattern holds it, so the state after it is
@@ -1843,6 +1846,13 @@ __global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
     }
 }
 
+// A value every lane of the wave holds, in scalar registers.
+__device__ __forceinline__ int64_t wave_uniform64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)((uint64_t)hi << 32 | lo);
+}
+
 // ---- the fallback-linked (FL) form (pm_flatten.h, pm_pack_sparse_fl) -----
 // The 8-B form's record holds its fallback row, so it has no room for the
 // record's own output: record states whose output is past the inline code
@@ -1871,7 +1881,7 @@ static_assert(PM_FL_SPEC == 0 || PM_FL_SPEC == 2, "PM_FL_SPEC: 0 (product) or 2 
 // A lane holds the aligned block of records its state is in (16 or 32 B:
 // one or two 16-B loads; PM_FL_BLK, an ablation switch of build_ab.sh).
 #ifndef PM_FL_BLK
-#define PM_FL_BLK 16
+#define PM_FL_BLK 32
 #endif
 static_assert(PM_FL_BLK == 16 || PM_FL_BLK == 32, "PM_FL_BLK: 16 or 32");
 constexpr uint32_t FL_BLK_SHIFT = PM_FL_BLK == 16 ? 1u : 2u;  // granules per block: 2 or 4
@@ -1952,16 +1962,21 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
 
 // The FL form's scan: the staged-id structure of dfa_sparse_stage16_kernel
 // (u16 staging rows, escapes in rounds, whole-line non-temporal stores;
-// 1,024-lane workgroups, the KR shallowest rows in LDS), the FL step, and outputs one step late: a step writes the
-// output of the position before it (the state it starts from holds it).
-template <int KR, bool NT = true>
+// 1,024-lane workgroups, the KR shallowest rows in LDS), the FL step, and
+// outputs one step late: a step writes the output of the position before it
+// (the state it starts from holds it).  OUTW 4 / 2: u32 / u16 ids (a u16
+// block of a chain is 64 B: four lanes' 16-B stores, 16 chains per store
+// instruction); 0: the count alone, no staging rows, no escapes, no stores.
+template <int KR, int OUTW = 4>
 __global__ __launch_bounds__(1024) void dfa_fl_kernel(
-    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* __restrict__ out,
+    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
     const uint16_t* __restrict__ rowout16, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
+    static_assert(OUTW == 0 || OUTW == 2 || OUTW == 4, "u32 / u16 ids or the count");
     constexpr int THREADS = 1024, BLK = 32, SROW = 17;
+    constexpr bool kIds = OUTW != 0;
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
-    __shared__ uint32_t s_ids[THREADS * SROW];
+    __shared__ uint32_t s_ids[kIds ? THREADS * SROW : 1];
     {
         const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
         const uint4* src = reinterpret_cast<const uint4*>(base);
@@ -1970,14 +1985,20 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
-    uint16_t* const my = reinterpret_cast<uint16_t*>(s_ids + threadIdx.x * SROW);
-    const uint32_t* const wrows = s_ids + (threadIdx.x - lane) * SROW;  // the wave's rows
+    uint16_t* const my = reinterpret_cast<uint16_t*>(s_ids + (kIds ? threadIdx.x * SROW : 0));
+    const uint32_t* const wrows = s_ids + (kIds ? (threadIdx.x - lane) * SROW : 0);  // the wave's rows
     const int64_t nseg = (n + seg_len - 1) / seg_len;
     const int64_t lanes = (int64_t)gridDim.x * THREADS;
     uint32_t cnt = 0, cb = 0xFFFFFFFFu, own = 0;
     tu32x4 R0 = {0u, 0u, 0u, 0u}, R1 = {0u, 0u, 0u, 0u};
     for (int64_t sg0 = (int64_t)blockIdx.x * THREADS + threadIdx.x; __ballot(sg0 < nseg); sg0 += lanes) {
         const bool has = sg0 < nseg;
+        // the wave's segments are consecutive: a wave-uniform 64-bit base
+        // (scalar registers) and 32-bit lane offsets for the text loads and
+        // the stores
+        const int64_t wseg = wave_uniform64(sg0 - lane);
+        const uint32_t sl = (uint32_t)seg_len;
+        const uint8_t* const tbase = text + pos0 + wseg * seg_len;
         const int64_t lo = has ? pos0 + sg0 * seg_len : pos0 + n;
         const int64_t hi = has ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : pos0 + n;
         int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
@@ -1993,7 +2014,8 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 act[tt] = lo + BLK * (b0 + tt) + BLK <= hi;
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
-                    const tu32x4* tp = reinterpret_cast<const tu32x4*>(text + lo + BLK * (b0 + tt) + 16 * q);
+                    const tu32x4* tp = reinterpret_cast<const tu32x4*>(
+                        tbase + ((uint32_t)lane * sl + (uint32_t)(BLK * (b0 + tt) + 16 * q)));
                     const tu32x4 v = act[tt] ? *tp : tu32x4{0u, 0u, 0u, 0u};
                     WT[tt][4 * q] = v.x;
                     WT[tt][4 * q + 1] = v.y;
@@ -2016,8 +2038,10 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                         const uint32_t code = w >> 20;
                         const bool esc = !rec && code == DFA_ESC;
                         const uint32_t id = rec ? own : code;
-                        my[j - 1] = (uint16_t)(esc ? (w & DFA_STATE_MASK) : id);
-                        em |= esc ? 1u << (j - 1) : 0u;
+                        if (kIds) {
+                            my[j - 1] = (uint16_t)(esc ? (w & DFA_STATE_MASK) : id);
+                            em |= esc ? 1u << (j - 1) : 0u;
+                        }
                         cnt += act[tt] && id != 0u;  // an escape is a nonzero id
                     }
                     w = act[tt] ? wn : w;
@@ -2025,10 +2049,13 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 {  // position 31
                     bool esc;
                     const uint32_t id = fl_output(base, F, w, cb, R0, R1, esc);
-                    my[BLK - 1] = (uint16_t)(esc ? (w & DFA_STATE_MASK) : id);
-                    em |= esc ? 1u << (BLK - 1) : 0u;
+                    if (kIds) {
+                        my[BLK - 1] = (uint16_t)(esc ? (w & DFA_STATE_MASK) : id);
+                        em |= esc ? 1u << (BLK - 1) : 0u;
+                    }
                     cnt += act[tt] && id != 0u;
                 }
+                if (!kIds) return;
                 if (!act[tt]) em = 0;
                 while (__ballot(em != 0)) {  // row outputs past the inline code: one per lane per round
                     if (em) {
@@ -2038,19 +2065,40 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
+                // Store instruction t writes chain cc = CPI * t + lane / LPC
+                // (LPC lanes of 16 B each per chain block): whole lines.  The
+                // lane's LDS and output offsets are laundered per block so
+                // the compiler forms each store's addresses from one register
+                // and an immediate / scalar step (hoisted out of the block
+                // loop, eight of each spilled, and their reloads waited for
+                // every store in flight)
+                constexpr int LPC = OUTW == 4 ? 8 : 4, CPI = 64 / LPC, NST = 64 / CPI;
                 const uint64_t am = __ballot(act[tt]);
-                uint32_t* o = out + (sg0 - lane + (lane >> 3)) * seg_len + BLK * b + 4 * (lane & 7);
+                uint32_t lds_off = ((uint32_t)(lane / LPC) * SROW + (OUTW == 4 ? 2u : 4u) * (lane % LPC)) * 4u;
+                uint32_t go = (uint32_t)(lane / LPC) * sl + (uint32_t)(16 / OUTW) * (lane % LPC);
+                asm volatile("" : "+v"(lds_off), "+v"(go));
+                const uint64_t mine = am >> (lane / LPC);  // bit CPI * t: chain of store t active
+                const bool full = am == ~0ull;
+                const uint8_t* const lb = reinterpret_cast<const uint8_t*>(wrows) + lds_off;
+                tu32x4 vs[NST];  // every store's ids read first (one LDS wait), inactive chains too
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const int cc = 8 * t + (lane >> 3);
-                    const uint32_t* src = wrows + cc * SROW + 2 * (lane & 7);
-                    const uint32_t w0 = src[0], w1 = src[1];
-                    const tu32x4 v = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
-                    if ((am >> cc) & 1u) {
-                        if (NT) __builtin_nontemporal_store(v, reinterpret_cast<tu32x4*>(o));
-                        else *reinterpret_cast<tu32x4*>(o) = v;
+                for (int t = 0; t < NST; ++t) {
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(lb + t * CPI * SROW * 4);
+                    if (OUTW == 4) {
+                        const uint32_t w0 = src[0], w1 = src[1];
+                        vs[t] = tu32x4{w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
+                    } else {
+                        vs[t] = tu32x4{src[0], src[1], src[2], src[3]};
                     }
-                    o += 8 * seg_len;
+                }
+#pragma unroll
+                for (int t = 0; t < NST; ++t) {
+                    const tu32x4 v = vs[t];
+                    const int64_t step = (int64_t)(CPI * t) * seg_len + BLK * b;  // wave-uniform
+                    tu32x4* o = OUTW == 4
+                                    ? reinterpret_cast<tu32x4*>(reinterpret_cast<uint32_t*>(out) + wseg * seg_len + step + go)
+                                    : reinterpret_cast<tu32x4*>(reinterpret_cast<uint16_t*>(out) + wseg * seg_len + step + go);
+                    if (full || ((mine >> (CPI * t)) & 1u)) __builtin_nontemporal_store(v, o);
                 }
                 __builtin_amdgcn_wave_barrier();
             });
@@ -2060,8 +2108,9 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
             w = fl_step<KR>(base, F, s_rows, w, text[i], cb, R0, R1, own);
             bool esc;
             uint32_t id = fl_output(base, F, w, cb, R0, R1, esc);
-            if (esc) id = rowout16[w & DFA_STATE_MASK];
-            out[i - pos0] = id;
+            if (kIds && esc) id = rowout16[w & DFA_STATE_MASK];
+            if (OUTW == 4) reinterpret_cast<uint32_t*>(out)[i - pos0] = id;
+            if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[i - pos0] = (uint16_t)id;
             cnt += id != 0u;
         }
     }
@@ -2342,31 +2391,29 @@ constexpr int SDFA_LANES_PER_CU = 1024, SDFA_BLK = 32;
 // 0.07, 16 MiB 0.76-0.86 -> 0.28-0.37, 64 MiB 1.06-1.43 -> 0.59-0.73;
 // scripts/dfa_seg_sweep.py, profiles/r02/dfa_segment_sweep.txt).
 //
-// Product kernels of the sparse form, by output width (DfaDev::sparse_kernel
-// 0; side by side histories in DESIGN.md §4):
-//   u32 ids    the fallback-linked form (dfa_fl_kernel, PM_SK_FL); without
-//              it (>= 65,536 rows) the u16-staged 8-B-unit kernel
-//              (dfa_sparse_stage16_kernel<88, 4>, PM_SK_STAGE16); with gids
-//              past u16 the u32-staged one (dfa_sparse_stage_kernel,
-//              PM_SK_STAGE); without 8-B units (ids past 2^20) the lock-step
-//              kernel over the 16-B records (PM_SK_LOCK16)
-//   u16 ids    the lock-step kernel over 8-B units with the root and the 63
-//              shallowest rows in LDS (PM_SK_LOCK8), else PM_SK_LOCK16
-//   count      the lock-step kernel over 8-B units without LDS rows
-//              (PM_SK_LOCK8), else PM_SK_LOCK16
+// Product kernels of the sparse form (DfaDev::sparse_kernel 0; side by side
+// histories in DESIGN.md §4): the fallback-linked form (dfa_fl_kernel,
+// PM_SK_FL) at every width -- u32 / u16 ids staged in LDS, or the count
+// alone -- where the object has it (< 65,536 rows and gids); else for u32
+// ids the u16-staged 8-B-unit kernel (dfa_sparse_stage16_kernel<88, 4>,
+// PM_SK_STAGE16), with gids past u16 the u32-staged one (PM_SK_STAGE); for
+// u16 ids and the count the lock-step kernel over 8-B units (PM_SK_LOCK8);
+// without 8-B units (ids past 2^20) the lock-step kernel over the 16-B
+// records (PM_SK_LOCK16).
 // A forced kernel (DfaDev::sparse_kernel; tests, A/B timing) runs where the
 // object has its image and it writes the width asked for; other launches
 // take the product choice (pm_dfa_sparse_choice reports which ran).
 int pm_dfa_sparse_choice(const DfaDev& t, int outw) {
     if (!(t.coded && t.sbase && t.form != 1)) return 0;
     const int sk = t.sparse_kernel;
-    const bool ok = sk == PM_SK_FL       ? t.flbase && outw == 4
+    const bool ok = sk == PM_SK_FL       ? t.flbase != nullptr
                     : sk == PM_SK_STAGE16 ? t.sout8h && outw == 4
                     : sk == PM_SK_STAGE   ? t.sbase8 && outw != 0
                     : sk == PM_SK_LOCK8   ? t.sbase8 != nullptr
                                           : sk == PM_SK_LOCK16;
     if (ok) return sk;
-    return outw == 4 ? (t.flbase ? PM_SK_FL : t.sout8h ? PM_SK_STAGE16 : t.sbase8 ? PM_SK_STAGE : PM_SK_LOCK16)
+    if (t.flbase) return PM_SK_FL;
+    return outw == 4 ? (t.sout8h ? PM_SK_STAGE16 : t.sbase8 ? PM_SK_STAGE : PM_SK_LOCK16)
                      : (t.sbase8 ? PM_SK_LOCK8 : PM_SK_LOCK16);
 }
 
@@ -2400,9 +2447,15 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         const dim3 gs((unsigned)wg), bs(wgt);
         switch (sk) {
             case PM_SK_FL:
-                hipLaunchKernelGGL((dfa_fl_kernel<FL_LDS_ROWS, true>), gs, bs, 0, s, text, stream_start, pos0, n,
-                                   reinterpret_cast<uint32_t*>(out), count, t.flbase, t.flF, t.flrowout16, t.warm, seg,
-                                   g3);
+                if (outw == 4)
+                    hipLaunchKernelGGL((dfa_fl_kernel<FL_LDS_ROWS, 4>), gs, bs, 0, s, text, stream_start, pos0, n, out,
+                                       count, t.flbase, t.flF, t.flrowout16, t.warm, seg, g3);
+                else if (outw == 2)
+                    hipLaunchKernelGGL((dfa_fl_kernel<FL_LDS_ROWS, 2>), gs, bs, 0, s, text, stream_start, pos0, n, out,
+                                       count, t.flbase, t.flF, t.flrowout16, t.warm, seg, g3);
+                else
+                    hipLaunchKernelGGL((dfa_fl_kernel<FL_COUNT_LDS_ROWS, 0>), gs, bs, 0, s, text, stream_start, pos0,
+                                       n, out, count, t.flbase, t.flF, t.flrowout16, t.warm, seg, g3);
                 break;
             case PM_SK_STAGE16:
                 hipLaunchKernelGGL((dfa_sparse_stage16_kernel<88, 4, true>), gs, bs, 0, s, text, stream_start, pos0, n,

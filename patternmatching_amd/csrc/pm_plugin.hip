@@ -108,18 +108,6 @@ constexpr size_t PIPE_ID_POSITIONS = (size_t)8 << 20;
 // gid path 37% slower (profiles/r02/host_path_small_staging_ab.txt).
 constexpr size_t PIPE_SMALL_POSITIONS = (size_t)256 << 10;
 
-// A small read_block launch captured as a HIP graph (scan_host): the launch
-// a key names, replayed while calls repeat it.  The key: candidate kernel,
-// stream start, first position, positions, output width, zero-copy flags;
-// the buffers are the slot's own (a reallocated slot drops its graphs).
-constexpr int SLOT_GRAPHS = 4;
-struct SlotGraph {
-    hipGraphExec_t exec = nullptr;
-    int64_t key[6] = {};
-    uint64_t used = 0;
-    int sparse_kernel = 0;  // the PmSparseKernel it launches (pm_hip_sparse_kernel_last)
-};
-
 // One pipeline slot: pinned host and device staging for one block and its
 // own stream, so two blocks are in flight.
 struct PipeSlot {
@@ -138,17 +126,7 @@ struct PipeSlot {
     bool timed = false;     // ev0 / ev1 bracket the launch (device seconds)
     int w = 4;              // bytes per result position in h_res / d_res
     size_t off = 0, m = 0;  // block = positions [off, off + m) of the call
-    SlotGraph graph[SLOT_GRAPHS];
-    uint64_t graph_tick = 0;
-    int64_t seen[6] = {-1, 0, 0, 0, 0, 0};  // the previous small launch's key (captured when repeated)
 };
-
-void drop_graphs(PipeSlot& q) {
-    for (SlotGraph& g : q.graph)
-        if (g.exec) (void)hipGraphExecDestroy(g.exec);
-    for (SlotGraph& g : q.graph) g = SlotGraph();
-    q.seen[0] = -1;
-}
 
 // RT scratch of the scan_device launches on one stream.  Launches on one
 // stream are ordered, so they share it; launches on different streams may
@@ -173,18 +151,18 @@ struct StreamSpill {
 //                (PM_HOST_GID16, default 0: the link wait shrinks 3 us, the
 //                widening costs 5 us more than the copy)
 //   host_events  small calls bracket their launch with timing events for
-//                pm_hip_device_seconds (PM_HOST_SMALL_EVENTS, default 1;
-//                without them a call saves ~2 us of ~40, and the CLI's device
-//                columns report small calls as unmeasured);
-//                profiles/r04/host_path/small_call_variants_ab.json
+//                pm_hip_device_seconds (PM_HOST_SMALL_EVENTS, default 0:
+//                the two events cost 7 us of a 43-us 100 KiB call,
+//                profiles/r05/small_call/; without them device_seconds is -1
+//                after a small call, and the CLI, which reports device time,
+//                turns them on for its objects)
 //   host_pool    small calls copy / map their results on the process's host
 //                pool (1, default) or on the calling thread alone (0)
-//   host_graph   a small call whose launch repeats the previous one's replays
-//                it from a captured HIP graph (PM_HOST_GRAPH, default 1):
-//                profiles/r05/small_call_probe.json put a 100 KiB
-//                zero-copy launch + wait at 23.5 us direct, 9.5 replayed
+// (Measured and removed, round 5: small calls replayed from captured HIP
+// graphs -- 100 KiB gids 43.3 -> 51.2 us per call, a replayed zero-copy
+// launch + wait 24.0 -> 38.0 us; profiles/r05/small_call/.)
 struct HostOpts {
-    int spin = -1, gid16 = -1, events = -1, pool = -1, graph = -1;
+    int spin = -1, gid16 = -1, events = -1, pool = -1;
 };
 struct PmHip {
     int kind_req = KIND_RT;
@@ -295,7 +273,6 @@ PmHip* create(int kind) {
 }
 
 void free_slot(PipeSlot& q) {
-    drop_graphs(q);
     if (q.d_stage) {
         (void)hipFree(q.d_stage);
         (void)hipFree(q.d_res);
@@ -684,74 +661,6 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
     return e;
 }
 
-// The candidate kernel a launch through ap runs without measuring anything,
-// or -1 when this launch measures or tries a form: the RT kind's kernel, an
-// AC object's only or forced form, or a held auto / AC choice (the launch
-// spends one of the hold's launches here).
-int fixed_cand(PmHip* o, AutoPick& ap) {
-    if (o->kind == KIND_RT) return CAND_RT;
-    if (o->kind == KIND_AC && (!o->dfa.sbase || o->dfa_form))
-        return o->dfa.sbase && o->dfa_form != 1 ? CAND_SPARSE : CAND_DENSE;
-    init_pick(ap, o->kind, o->dfa.sbase != nullptr);
-    resolve_pick(o, ap);
-    if (ap.hold > 0) {
-        --ap.hold;
-        return ap.chosen;
-    }
-    return -1;
-}
-
-// A small read_block launch (host_graph): the first launch of a key runs
-// directly; when the next call repeats it (the reference's fixed-size
-// chunks, measure.c:284, repeat one key from the second chunk on) it is
-// captured into a graph on the slot, which later calls replay -- one
-// hipGraphLaunch instead of the launcher's argument setup and dispatch.
-// Launches that measure (auto / AC picks) always run directly.
-hipError_t launch_small(PmHip* o, PipeSlot& q, const uint8_t* text, int64_t ss, int64_t p0, int64_t n, void* out,
-                        int flags) {
-    const int c = fixed_cand(o, q.pick);
-    if (c < 0) return launch(o, text, ss, p0, n, out, q.w, nullptr, q.stream, q.spill, q.spill_cap, q.pick);
-    RtDev t = o->rt;
-    t.spill = q.spill;
-    t.spill_cap = q.spill_cap;
-    const int64_t key[6] = {c, ss, p0, n, q.w, flags};
-    auto same = [&](const int64_t* k) { return std::equal(key, key + 6, k); };
-    SlotGraph* g = nullptr;
-    for (SlotGraph& x : q.graph)
-        if (x.exec && same(x.key)) g = &x;
-    if (!g && !same(q.seen)) {
-        std::copy(key, key + 6, q.seen);
-        return launch_cand(o, q.pick, c, text, ss, p0, n, out, q.w, nullptr, q.stream, t);
-    }
-    if (!g) {  // repeated: capture it in the least recently used entry
-        g = &q.graph[0];
-        for (SlotGraph& x : q.graph)
-            if (x.used < g->used) g = &x;
-        if (g->exec) (void)hipGraphExecDestroy(g->exec);
-        *g = SlotGraph();
-        hipGraph_t gr = nullptr;
-        hipError_t e = hipStreamBeginCapture(q.stream, hipStreamCaptureModeThreadLocal);
-        if (e != hipSuccess) return e;
-        const hipError_t el = launch_cand(o, q.pick, c, text, ss, p0, n, out, q.w, nullptr, q.stream, t);
-        e = hipStreamEndCapture(q.stream, &gr);
-        if (el != hipSuccess) e = el;
-        if (e == hipSuccess) e = hipGraphInstantiate(&g->exec, gr, nullptr, nullptr, 0);
-        if (gr) (void)hipGraphDestroy(gr);
-        if (e != hipSuccess) {
-            g->exec = nullptr;
-            return e;
-        }
-        std::copy(key, key + 6, g->key);
-        g->sparse_kernel = o->last_sparse_kernel;
-    } else {  // what launch_cand notes at a direct launch
-        q.pick.last = c == CAND_RT ? KIND_RT : KIND_AC;
-        q.pick.last_form = c == CAND_RT ? 0 : c == CAND_SPARSE ? 2 : 1;
-        if (c != CAND_RT) o->last_sparse_kernel = g->sparse_kernel;
-    }
-    g->used = ++q.graph_tick;
-    return hipGraphLaunch(g->exec, q.stream);
-}
-
 // Scan n new bytes after the carried history.  Results go to out_gid (gids)
 // or out_ids (the caller's pattern ids, PM_NULL_PATTERN_ID for none) -- one
 // of the two is non-null.  Blocks alternate between two slots (streams):
@@ -794,8 +703,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
     if (g_hprof_on) g_hprof[4] += 1;
     const bool pool = o->hopt.pool != 0;  // (the pool's size: PM_HOST_POOL)
     const bool gid16 = opt_or_env(o->hopt.gid16, "PM_HOST_GID16", 0);
-    const bool events = opt_or_env(o->hopt.events, "PM_HOST_SMALL_EVENTS", 1);
-    const bool graphs = opt_or_env(o->hopt.graph, "PM_HOST_GRAPH", 1);
+    const bool events = opt_or_env(o->hopt.events, "PM_HOST_SMALL_EVENTS", 0);
     auto finish = [&](PipeSlot& q) {
         lap(1);
         if (opt_or_env(o->hopt.spin, "PM_HOST_SPIN", 0)) {
@@ -877,12 +785,8 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         if (q.timed) PM_CHECK(hipEventRecord(q.ev0, q.stream));
         const uint8_t* text = zc_in ? q.h_stage : q.d_stage;
         void* res = zc_out ? q.h_res : q.d_res;
-        if (q.staged && graphs)
-            PM_CHECK(launch_small(o, q, text, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, res,
-                                  (zc_in ? 1 : 0) | (zc_out ? 2 : 0)));
-        else
-            PM_CHECK(launch(o, text, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, res, q.w, nullptr, q.stream,
-                            q.spill, q.spill_cap, q.pick));
+        PM_CHECK(launch(o, text, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, res, q.w, nullptr, q.stream, q.spill,
+                        q.spill_cap, q.pick));
         o->last_kernel = q.pick.last ? q.pick.last : o->kind;
         o->last_form = q.pick.last_form;
         o->last_out_width = q.w;
@@ -1286,7 +1190,6 @@ int pm_hip_set_option(void* obj, const char* name, int64_t value) {
     PmHip* o = as(obj);
     if (!name) return -1;
     const std::string k(name);
-    for (PipeSlot& q : o->slot) drop_graphs(q);  // captured launches may no longer be what a launch would run
     auto flag = [&](int& dst) {  // -1 = the environment's default, 0 / 1
         if (value < -1 || value > 1) return -1;
         dst = (int)value;
@@ -1323,7 +1226,6 @@ int pm_hip_set_option(void* obj, const char* name, int64_t value) {
     if (k == "host_gid16") return flag(o->hopt.gid16);
     if (k == "host_events") return flag(o->hopt.events);
     if (k == "host_pool") return flag(o->hopt.pool);
-    if (k == "host_graph") return flag(o->hopt.graph);
     return -1;
 }
 

@@ -12,9 +12,8 @@ microseconds per call (median of 300, snort, RT kind, ASCII):
   graph_zc           kernel_zc captured once into a HIP graph, then replayed
   write_zc_400k      a device copy of 400 KB into pinned host memory + sync
                      (the link's share: the ids a call brings back)
-  read_block_gid     the whole call (staging, launch, wait, result copy),
-                     its launch replayed from a captured HIP graph (the
-                     "host_graph" option, default on); _nograph: option off
+  read_block_gid     the whole call (staging, launch, wait, result copy);
+                     _events: with the per-call timing events (host_events)
   read_block_ids     the same for pattern ids (read_block; ac kind too)
   host_copy_400k     memcpy of 400 KB pinned -> pageable on the host
 Prints one JSON object."""
@@ -95,7 +94,8 @@ hout.zero_()
 
 
 def graph_zc():
-    g.replay()
+    with torch.cuda.stream(s):  # (replay() launches on the current stream)
+        g.replay()
     s.synchronize()
 
 
@@ -131,9 +131,9 @@ def call_ids(mm):
 ac = pm.HipMatcher("ac")
 ac.add_dictionary(d)
 ac.compile()
-for g, tag in ((1, ""), (0, "_nograph")):
+for ev, tag in ((0, ""), (1, "_events")):
     for mm, kname in ((m, ""), (ac, "_ac")):
-        assert mm.set_option("host_graph", g) == 0
+        assert mm.set_option("host_events", ev) == 0
         mm.reset()
         fn = call if mm is m else (lambda: lib.pm_hip_read_block_gid(
             ac.obj, part.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), N,
@@ -141,6 +141,7 @@ for g, tag in ((1, ""), (0, "_nograph")):
         res[f"read_block_gid{kname}{tag}_us"] = timeit(fn)
         mm.reset()
         res[f"read_block_ids{kname}{tag}_us"] = timeit(call_ids(mm))
+        mm.set_option("host_events", -1)
     res[f"read_block_gid{tag}_GBps"] = round(N / res[f"read_block_gid{tag}_us"] / 1e3, 3)
 dst = np.empty(N, np.int32)
 hn = hout.numpy()
