@@ -558,23 +558,54 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
     const uint32_t keep = std::min(F, PM_FL_LDS_ROWS);
     std::stable_sort(ord.begin() + keep, ord.end(), [&](uint32_t a, uint32_t b) { return use[a] > use[b]; });
     for (uint32_t k = 0; k < F; ++k) nrow[ord[k]] = k;
-    // folded slotless records; granules of the others
+    // trie depth of every state, breadth first from the root: a row's
+    // entries hold its goto children, a record's slots are all of its own
+    // (a goto child differs from the fallback's transition: it is deeper)
+    std::vector<uint16_t> dep(S, 0xFFFFu);
+    {
+        std::vector<uint32_t> q(1, 0u);
+        dep[0] = 0;
+        for (size_t h = 0; h < q.size(); ++h) {
+            const uint32_t v = q[h];
+            auto visit = [&](uint32_t t) {
+                if (dep[t] == 0xFFFFu) {
+                    dep[t] = (uint16_t)std::min<uint32_t>(dep[v] + 1u, 0xFFFEu);
+                    q.push_back(t);
+                }
+            };
+            if (v < F) {
+                for (uint32_t c = 0; c < 256; ++c) visit(d.sblock[(size_t)v * 256 + c] & PM_DFA_STATE_MASK);
+            } else {
+                const uint32_t* r = R(v);
+                if (r[0] & 0x100u) visit(r[1] & PM_DFA_STATE_MASK);
+                if (r[0] & 0x1000000u) visit(r[2] & PM_DFA_STATE_MASK);
+            }
+        }
+    }
+    // folded slotless records; granules of the others, shallow part first
     std::vector<uint8_t> fold(S, 0);
     std::vector<uint32_t> gid(S, 0);  // granule of a record
     uint64_t u = 0;
-    for (uint32_t v = F; v < S; ++v) {
-        const uint32_t* r = R(v);
-        const bool s0 = r[0] & 0x100u, s1 = r[0] & 0x1000000u;
-        if (!s0 && d.sout[v] < PM_DFA_ESC) {
-            fold[v] = 1;
-            ++fl.folded;
-            continue;
+    for (int part = 0; part < 2; ++part) {
+        if (part == 1) {
+            u = (u + 3) & ~(uint64_t)3;  // the deep part starts a 32-B block
+            fl.deep_g = (uint32_t)u;
         }
-        const bool wide = s1 || nrow[r[3]] >= PM_FL_FB_INREC;
-        if (wide && (u & 1)) ++u;  // 16 B at a 16-B boundary (the kernel's blocks: 16 or 32 B)
-        gid[v] = (uint32_t)u;
-        u += wide ? 2 : 1;
-        if (F + u > PM_DFA_STATE_MASK + 1) return false;
+        for (uint32_t v = F; v < S; ++v) {
+            if ((dep[v] >= PM_FL_DEEP_DEPTH) != (part == 1)) continue;
+            const uint32_t* r = R(v);
+            const bool s0 = r[0] & 0x100u, s1 = r[0] & 0x1000000u;
+            if (!s0 && d.sout[v] < PM_DFA_ESC) {
+                fold[v] = 1;
+                ++fl.folded;
+                continue;
+            }
+            const bool wide = s1 || nrow[r[3]] >= PM_FL_FB_INREC;
+            if (wide && (u & 1)) ++u;  // 16 B at a 16-B boundary
+            gid[v] = (uint32_t)u;
+            u += wide ? 2 : 1;
+            if (F + u > PM_DFA_STATE_MASK + 1) return false;
+        }
     }
     fl.F = F;
     fl.granules = (uint32_t)u;

@@ -199,10 +199,19 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
 // the 20-bit target field.
 constexpr uint32_t PM_FL_FB_INREC = 4095;  // the 12-bit field's top value
 constexpr uint32_t PM_FL_LDS_ROWS = 88;  // rows the kernel stages in LDS (dfa_fl_kernel<88>)
+// Records of trie depth < PM_FL_DEEP_DEPTH come first (the kernel loads
+// them as 16-B halves: a walk rarely stays), then, from granule deep_g (a
+// multiple of 4), the deeper ones (loaded as aligned 32-B blocks: a walk
+// that got this deep is usually on a pattern's unary run, whose records
+// follow each other).  Within each part, the trie's order.
+#ifndef PM_FL_DEEP_DEPTH
+#define PM_FL_DEEP_DEPTH 4
+#endif
 struct FlImage {
     std::vector<uint32_t> block;     // F * 256 row words, then 2 words per granule
     std::vector<uint16_t> rowout16;  // output of each row (escapes)
     uint32_t F = 0, granules = 0, folded = 0;
+    uint32_t deep_g = 0;             // first granule of the deep records
 };
 bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl);
 // One FL step from state s with the word w that led to it (w = 0 at the

@@ -73,6 +73,7 @@ struct DfaDev {
     const uint8_t* flbase;
     const uint16_t* flrowout16;
     uint32_t flF;
+    uint32_t flGD;  // first deep granule (pm_flatten.h FlImage::deep_g)
 };
 
 // Positions [pos0, pos0+n) of text; bytes back to stream_start are context.

@@ -1878,23 +1878,30 @@ __device__ __forceinline__ int64_t wave_uniform64(int64_t v) {
 #endif
 static_assert(PM_FL_SPEC == 0 || PM_FL_SPEC == 2, "PM_FL_SPEC: 0 (product) or 2 (ablation)");
 
-// A lane holds the aligned block of records its state is in (16 or 32 B:
-// one or two 16-B loads; PM_FL_BLK, an ablation switch of build_ab.sh).
-#ifndef PM_FL_BLK
-#define PM_FL_BLK 32
-#endif
-static_assert(PM_FL_BLK == 16 || PM_FL_BLK == 32, "PM_FL_BLK: 16 or 32");
-constexpr uint32_t FL_BLK_SHIFT = PM_FL_BLK == 16 ? 1u : 2u;  // granules per block: 2 or 4
+// A lane holds the records around its state: for a shallow record (granule
+// below GD, pm_flatten.h FlImage::deep_g) the 16-B half holding it, in R0;
+// for a deep one the aligned 32-B block, R0 and R1.  The held key: the
+// half's index, or the block's with the top bit set.
+__device__ __forceinline__ uint32_t fl_key(uint32_t g, bool deep) { return deep ? (g >> 2) | 0x80000000u : g >> 1; }
+
+__device__ __forceinline__ void fl_load(const uint8_t* __restrict__ base, uint32_t F, uint32_t g, bool deep,
+                                        tu32x4& R0, tu32x4& R1) {
+    const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + ((g >> 1) & (deep ? ~1u : ~0u)) * 16u);
+    R0 = p[0];
+    if (deep) R1 = p[1];
+}
 
 template <int KR>
-__device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, uint32_t F,
+__device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
                                             const uint32_t* __restrict__ s_rows, uint32_t w, uint32_t c,
                                             uint32_t& cb, tu32x4& R0, tu32x4& R1, uint32_t& own) {
     const uint32_t s = w & DFA_STATE_MASK;
     const bool isrow = s < F;
-    const uint32_t g = s - F, blk = g >> FL_BLK_SHIFT;
+    const uint32_t g = s - F;
+    const bool deep = g >= GD;
+    const uint32_t key = fl_key(g, deep);
     const uint32_t fb = w >> 20;
-    const bool newblk = !isrow && blk != cb;
+    const bool newblk = !isrow && key != cb;
     const bool pre = PM_FL_SPEC == 2 && newblk && fb != PM_FL_INREC && fb >= (uint32_t)KR;
     const bool lrow = isrow && s < (uint32_t)KR;
     // the global word: a row state's word (or, PM_FL_SPEC 2, a new
@@ -1902,28 +1909,17 @@ __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, ui
     uint32_t x = 0;
     if ((isrow && !lrow) || pre) x = *reinterpret_cast<const uint32_t*>(base + (bsel(bmask(isrow), fb, s) * 1024u + c * 4u));
     if (newblk) {
-        const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * (uint32_t)PM_FL_BLK);
-        R0 = p[0];
-        if (PM_FL_BLK == 32) R1 = p[1];
-        cb = blk;
+        fl_load(base, F, g, deep, R0, R1);
+        cb = key;
     }
     const uint32_t lw = s_rows[(bmask(lrow) & s) * 256u + c];  // (row 0 for the other lanes: no branch)
-    // words 2e .. 2e + 3 of the block, e the granule in it (a 16-B record
-    // starts at an even granule)
-    const uint32_t m1 = bmask(g & 1u);
-    uint32_t w0, w1, w2, w3;
-    if (PM_FL_BLK == 16) {
-        w0 = bsel(m1, R0.x, R0.z);
-        w1 = bsel(m1, R0.y, R0.w);
-        w2 = R0.z;
-        w3 = R0.w;
-    } else {
-        const uint32_t m2 = bmask(g & 2u);
-        w0 = bsel(m2, bsel(m1, R0.x, R0.z), bsel(m1, R1.x, R1.z));
-        w1 = bsel(m2, bsel(m1, R0.y, R0.w), bsel(m1, R1.y, R1.w));
-        w2 = bsel(m2, R0.z, R1.z);
-        w3 = bsel(m2, R0.w, R1.w);
-    }
+    // words 2e .. 2e + 3 of what the lane holds, e the granule in it (a
+    // 16-B record starts at an even granule)
+    const uint32_t m1 = bmask(g & 1u), m2 = bmask(deep && (g & 2u));
+    const uint32_t w0 = bsel(m2, bsel(m1, R0.x, R0.z), bsel(m1, R1.x, R1.z));
+    const uint32_t w1 = bsel(m2, bsel(m1, R0.y, R0.w), bsel(m1, R1.y, R1.w));
+    const uint32_t w2 = bsel(m2, R0.z, R1.z);
+    const uint32_t w3 = bsel(m2, R0.w, R1.w);
     own = w0 & 0xFFFFu;
     const bool h0 = c == ((w0 >> 16) & 0xFFu), h1 = c == (w0 >> 24);
     const uint32_t row = bsel(bmask(fb == PM_FL_INREC), fb, w3);
@@ -1937,26 +1933,26 @@ __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, ui
     return bsel(bmask(isrow), rec, bsel(bmask(lrow), x, lw));
 }
 
-// The output of the position that produced w: a record's own out16 (its
-// block loaded into R0 / R1 if the lane does not hold it -- the next step's
-// load, made early), or a row word's code; *esc = the code escapes (the
-// answer is then rowout16[w & MASK]).
-__device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, uint32_t F, uint32_t w, uint32_t& cb,
-                                              tu32x4& R0, tu32x4& R1, bool& esc) {
+// The output of the position that produced w: a record's own out16 (what
+// holds it loaded into R0 / R1 if the lane does not hold it -- the next
+// step's load, made early), or a row word's code; *esc = the code escapes
+// (the answer is then rowout16[w & MASK]).
+__device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, uint32_t F, uint32_t GD, uint32_t w,
+                                              uint32_t& cb, tu32x4& R0, tu32x4& R1, bool& esc) {
     const uint32_t s = w & DFA_STATE_MASK;
     esc = false;
     if (s < F) {
         esc = (w >> 20) == DFA_ESC;
         return w >> 20;
     }
-    const uint32_t g = s - F, blk = g >> FL_BLK_SHIFT;
-    if (blk != cb) {
-        const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + blk * (uint32_t)PM_FL_BLK);
-        R0 = p[0];
-        if (PM_FL_BLK == 32) R1 = p[1];
-        cb = blk;
+    const uint32_t g = s - F;
+    const bool deep = g >= GD;
+    const uint32_t key = fl_key(g, deep);
+    if (key != cb) {
+        fl_load(base, F, g, deep, R0, R1);
+        cb = key;
     }
-    const uint32_t w0 = (PM_FL_BLK == 32 && (g & 2u)) ? ((g & 1u) ? R1.z : R1.x) : ((g & 1u) ? R0.z : R0.x);
+    const uint32_t w0 = (deep && (g & 2u)) ? ((g & 1u) ? R1.z : R1.x) : ((g & 1u) ? R0.z : R0.x);
     return w0 & 0xFFFFu;
 }
 
@@ -1970,7 +1966,7 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
 template <int KR, int OUTW = 4>
 __global__ __launch_bounds__(1024) void dfa_fl_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
-    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
+    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
     const uint16_t* __restrict__ rowout16, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
     static_assert(OUTW == 0 || OUTW == 2 || OUTW == 4, "u32 / u16 ids or the count");
     constexpr int THREADS = 1024, BLK = 32, SROW = 17;
@@ -2004,7 +2000,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
         int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
         if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
         uint32_t w = 0;  // the root, reached by no word
-        for (int64_t i = wlo; i < lo; ++i) w = fl_step<KR>(base, F, s_rows, w, text[i], cb, R0, R1, own);
+        for (int64_t i = wlo; i < lo; ++i) w = fl_step<KR>(base, F, GD, s_rows, w, text[i], cb, R0, R1, own);
         const int64_t nblk = seg_len / BLK;
         for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
             bool act[2];
@@ -2031,7 +2027,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 uint32_t em = 0;
 #pragma unroll
                 for (int j = 0; j < BLK; ++j) {
-                    const uint32_t wn = fl_step<KR>(base, F, s_rows, w, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb,
+                    const uint32_t wn = fl_step<KR>(base, F, GD, s_rows, w, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb,
                                                     R0, R1, own);
                     if (j > 0) {  // the output of position j - 1, which produced w
                         const bool rec = (w & DFA_STATE_MASK) >= F;
@@ -2048,7 +2044,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 }
                 {  // position 31
                     bool esc;
-                    const uint32_t id = fl_output(base, F, w, cb, R0, R1, esc);
+                    const uint32_t id = fl_output(base, F, GD, w, cb, R0, R1, esc);
                     if (kIds) {
                         my[BLK - 1] = (uint16_t)(esc ? (w & DFA_STATE_MASK) : id);
                         em |= esc ? 1u << (BLK - 1) : 0u;
@@ -2105,9 +2101,9 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
         }
         // the segment's last (< BLK) positions
         for (int64_t i = lo + BLK * ((hi - lo) / BLK); i < hi; ++i) {
-            w = fl_step<KR>(base, F, s_rows, w, text[i], cb, R0, R1, own);
+            w = fl_step<KR>(base, F, GD, s_rows, w, text[i], cb, R0, R1, own);
             bool esc;
-            uint32_t id = fl_output(base, F, w, cb, R0, R1, esc);
+            uint32_t id = fl_output(base, F, GD, w, cb, R0, R1, esc);
             if (kIds && esc) id = rowout16[w & DFA_STATE_MASK];
             if (OUTW == 4) reinterpret_cast<uint32_t*>(out)[i - pos0] = id;
             if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[i - pos0] = (uint16_t)id;
@@ -2449,13 +2445,13 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
             case PM_SK_FL:
                 if (outw == 4)
                     hipLaunchKernelGGL((dfa_fl_kernel<FL_LDS_ROWS, 4>), gs, bs, 0, s, text, stream_start, pos0, n, out,
-                                       count, t.flbase, t.flF, t.flrowout16, t.warm, seg, g3);
+                                       count, t.flbase, t.flF, t.flGD, t.flrowout16, t.warm, seg, g3);
                 else if (outw == 2)
                     hipLaunchKernelGGL((dfa_fl_kernel<FL_LDS_ROWS, 2>), gs, bs, 0, s, text, stream_start, pos0, n, out,
-                                       count, t.flbase, t.flF, t.flrowout16, t.warm, seg, g3);
+                                       count, t.flbase, t.flF, t.flGD, t.flrowout16, t.warm, seg, g3);
                 else
                     hipLaunchKernelGGL((dfa_fl_kernel<FL_COUNT_LDS_ROWS, 0>), gs, bs, 0, s, text, stream_start, pos0,
-                                       n, out, count, t.flbase, t.flF, t.flrowout16, t.warm, seg, g3);
+                                       n, out, count, t.flbase, t.flF, t.flGD, t.flrowout16, t.warm, seg, g3);
                 break;
             case PM_SK_STAGE16:
                 hipLaunchKernelGGL((dfa_sparse_stage16_kernel<88, 4, true>), gs, bs, 0, s, text, stream_start, pos0, n,

@@ -919,6 +919,7 @@ void pm_hip_compile(void* obj) {
                 o->dfa.flbase = (const uint8_t*)dalloc_copy(o, fl.block.data(), fl.block.size() * 4);
                 o->dfa.flrowout16 = (const uint16_t*)dalloc_copy(o, fl.rowout16.data(), fl.rowout16.size() * 2);
                 o->dfa.flF = fl.F;
+                o->dfa.flGD = fl.deep_g;
             }
         }
     }
