@@ -1342,6 +1342,7 @@ struct PmFlatHandle {
     PmParents par;
     std::vector<uint32_t> block8, out8;  // pm_pack_sparse8 of the DFA's sparse form
     FlImage fl;                          // pm_pack_sparse_fl of it
+    std::vector<uint32_t> flinfo;        // pm_flat_array "flinfo"
     bool has_fl = false;
     int kind = 0;
     bool hit = false;
@@ -1397,6 +1398,10 @@ size_t pm_flat_array(void* handle, const char* name, const void** data, size_t* 
     if (s == "sout8") return ret(h->out8);
     if (s == "flblock") return ret(h->fl.block);
     if (s == "flrowout16") return ret(h->fl.rowout16);
+    if (s == "flinfo") {  // {F, granules, folded records, first deep granule}
+        h->flinfo = {h->fl.F, h->fl.granules, h->fl.folded, h->fl.deep_g};
+        return ret(h->flinfo);
+    }
     if (s == "index_of_gid") return ret(h->g.index_of_gid);
     if (s == "parent") return ret(h->par.parent);
     if (s == "depth") return ret(h->par.depth);

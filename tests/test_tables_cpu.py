@@ -345,3 +345,33 @@ def test_synchronizing_3gram_warmup(key):
             got = o.scan_codes(text[q:lo + 512])[lo - q:]
             assert np.array_equal(got, exact[lo:lo + 512]), (lo, q)
         assert synced > 0
+
+
+@pytest.mark.parametrize("key", ["et", "snort", "merged"])
+def test_fl_image_layout(key):
+    """The fallback-linked form's layout rules the device kernel relies on
+    (pm_flatten.h pm_pack_sparse_fl, dfa_fl_kernel): every 16-B record --
+    two slots, or a fallback row past the word's 12-bit field (the word then
+    holds 4095) -- starts at an even granule; the deep records start a
+    32-B block; every word's record target is a granule inside the image,
+    and a row target is a row."""
+    d, img, _ = image(key, pm.KIND_AC)
+    F, granules, folded, deep_g = (int(v) for v in img.array("flinfo"))
+    blk = img.array("flblock")
+    assert deep_g % 4 == 0 and deep_g <= granules and F > 0 and folded >= 0
+    assert len(blk) == F * 256 + 2 * granules
+    rec = blk[F * 256:].reshape(-1, 2)
+    rows = blk[:F * 256]
+    # the words: every row entry, and each record's slot words (word1; word2
+    # for the 16-B ones, found from the words that lead into them)
+    words = [rows, rec[:, 1]]
+    tgt = rows & 0xFFFFF
+    into_rec = rows[tgt >= F]
+    g = (into_rec & 0xFFFFF) - F
+    assert (g < granules).all()
+    w0 = rec[g, 0]
+    wide = (((w0 >> 16) & 0xFF) != (w0 >> 24)) | ((into_rec >> 20) == 4095)
+    assert (g[wide] % 2 == 0).all()
+    for w in words:
+        t = w & 0xFFFFF
+        assert ((t < F) | (t - F < granules)).all()
