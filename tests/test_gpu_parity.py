@@ -894,6 +894,48 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
 SPARSE_KERNELS = {1: (4, 2, 0), 2: (4,), 3: (4, 2), 4: (4, 2, 0), 5: (4, 2, 0)}
 
 
+def test_sparse_form_without_8b_units():
+    """An automaton inside the coded range whose 8-B record units do not fit
+    the coded word (F + units > 2^20: 200,000 random 8-byte patterns over
+    20 letters, 916,050 states -- larger than merged's) has the sparse form
+    but neither the 8-B nor the fallback-linked layout (gids past u16): its
+    u32 scans and its count take the lock-step kernel over the 16-B records
+    (sparse_kernel 5) and equal the dense rows' (no 8-B-unit
+    kernel may run on the missing image)."""
+    torch = _torch()
+    rng = np.random.default_rng(7)
+    pats = list({bytes(r) for r in (rng.integers(0, 20, size=(200000, 8)).astype(np.uint8) + ord("a"))})
+    m = pm.HipMatcher("ac")
+    m.add_dictionary(pm.Dictionary(patterns=pats))
+    m.compile()
+    n = 2 << 20
+    order = rng.integers(0, len(pats), size=n // 8 + 1)
+    text = np.frombuffer(b"".join(pats[k] for k in order), np.uint8)[:n].copy()
+    text[::97] = ord("z")  # breaks between pattern runs
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.from_numpy(np.concatenate([text, np.zeros(64, np.uint8)])).cuda()
+    try:
+        out = {}
+        for form in (1, 2):
+            assert m.set_option("dfa_form", form) == 0
+            a = torch.zeros(n, dtype=torch.int32, device="cuda")
+            c = torch.zeros(1, dtype=torch.int64, device="cuda")
+            m.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c.data_ptr(), s)
+            torch.cuda.synchronize()
+            if form == 2:
+                assert m.sparse_kernel_last == 5
+            cc = torch.zeros(1, dtype=torch.int64, device="cuda")
+            m.scan_device(dt.data_ptr(), 0, 0, n, 0, cc.data_ptr(), s)
+            torch.cuda.synchronize()
+            out[form] = (a, int(c.item()), int(cc.item()))
+        assert torch.equal(out[1][0], out[2][0])
+        assert out[1][1] == out[2][1] == out[1][2] == out[2][2] == int((out[1][0] != 0).sum().item())
+        assert out[1][1] > 0
+    finally:
+        m.set_option("dfa_form", 0)
+        m.free()
+
+
 @pytest.mark.parametrize("stream", ["lines", "ship"])
 def test_sparse_dfa_kernel_variants_agree(stream):
     """Every product kernel of the sparse form ("sparse_kernel" 1-5: the
@@ -1376,6 +1418,18 @@ def test_auto_stays_on_rt_for_sparse_matches():
         torch.cuda.synchronize()
         assert m.kernel_last == pm.KIND_RT
         assert torch.equal(got, want)
+    # small launches (<= 256 Ki positions: rt_small_kernel, whose deep
+    # signal counts only filter-passing candidates, as the chunked kernel's
+    # does): the reference's 100 KiB read_block chunks stay on RT too
+    text = dt[:4 << 20].cpu().numpy()
+    ref.reset()
+    want_ids = ref.read_block_gids(text)
+    m.reset()
+    got = []
+    for k in range(0, len(text), 100 << 10):
+        got.append(m.read_block_gids(text[k:k + (100 << 10)]))
+        assert m.kernel_last == pm.KIND_RT, k
+    assert np.array_equal(np.concatenate(got), want_ids)
 
 
 def test_auto_read_block_over_deep_then_sparse_blocks():
