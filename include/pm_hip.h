@@ -112,7 +112,8 @@ int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, un
 /* ac / auto kinds: keep the kernel picked for pm_hip_scan_device launches
  * (pm_hip_auto_create) for at least the next `launches` launches, so a timed
  * region never re-measures.  Returns the held kernel (1 = reverse trie,
- * 2 = AC dense rows, 3 = AC rows + records), 0 when the object has no choice
+ * 2 = AC dense rows, 3 = AC rows + records, 4 = the same with every record
+ * loaded as a 16-B half), 0 when the object has no choice
  * to make (rt kind, or a single DFA form), -1 while the pick is still being
  * measured (launch more, synchronize, and ask again). */
 int pm_hip_hold_choice(void* obj, int launches);

@@ -73,7 +73,12 @@ enum Kind { KIND_RT = 1, KIND_AC = 2, KIND_AUTO = 3 };
 constexpr double AUTO_SPILL_FRAC = 0.10;
 constexpr int AUTO_TRIAL = 2;
 constexpr int AUTO_HOLD = 64;
-enum Cand { CAND_RT = 0, CAND_DENSE = 1, CAND_SPARSE = 2, NCAND = 3 };
+// CAND_SPARSE16: the sparse form's fallback-linked kernel holding every
+// record as a 16-B half (FlImage::deep_g ignored): faster where walks
+// rarely stay in a record's block (the tiled shipped stream: 3.53 -> 3.36
+// ms, snort, profiles/r05/ab/fl_depth_split.jsonl), slower on the lines
+// stream (5.07 -> 5.54); timed beside the other forms.
+enum Cand { CAND_RT = 0, CAND_DENSE = 1, CAND_SPARSE = 2, CAND_SPARSE16 = 3, NCAND = 4 };
 
 struct AutoPick {
     unsigned long long* d_spill = nullptr;  // device counter of the last measured RT launch
@@ -82,7 +87,7 @@ struct AutoPick {
     hipEvent_t t0[NCAND] = {}, t1[NCAND] = {};  // timing of each candidate's measured launch
     bool pending = false;     // a measured RT launch (spill count + time) in flight
     bool timing = false;      // the DFA trials are launched, their times in flight
-    int queue[2] = {0, 0};    // DFA forms to try, in order
+    int queue[3] = {0, 0, 0};  // DFA forms to try, in order
     int nq = 0, qi = 0;       // forms queued / started
     int trial = 0;            // launches left of the form being tried (the last one timed)
     int64_t n_of[NCAND] = {};
@@ -533,10 +538,11 @@ void par_range(size_t n, size_t grain, const F& f) {
 hipError_t launch_cand(PmHip* o, AutoPick& ap, int c, const uint8_t* text, int64_t stream_start, int64_t pos0,
                        int64_t n, void* out, int outw, unsigned long long* count, hipStream_t s, const RtDev& t) {
     ap.last = c == CAND_RT ? KIND_RT : KIND_AC;
-    ap.last_form = c == CAND_RT ? 0 : c == CAND_SPARSE ? 2 : 1;
+    ap.last_form = c == CAND_RT ? 0 : c == CAND_DENSE ? 1 : 2;
     if (c == CAND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
     DfaDev d = o->dfa;
-    d.form = c == CAND_SPARSE ? 2 : 1;
+    d.form = c == CAND_DENSE ? 1 : 2;
+    if (c == CAND_SPARSE16) d.flGD = 0xFFFFFFFFu;
     o->last_sparse_kernel = pm_dfa_sparse_choice(d, out ? outw : 0);
     return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, d, o->num_cu, s);
 }
@@ -547,6 +553,9 @@ void start_trials(const PmHip* o, AutoPick& ap) {
     ap.nq = 0;
     if (o->dfa_form != 2 || !o->dfa.sbase) ap.queue[ap.nq++] = CAND_DENSE;
     if (o->dfa.sbase && o->dfa_form != 1) ap.queue[ap.nq++] = CAND_SPARSE;
+    if (o->dfa.flbase && o->dfa_form != 1 &&
+        (o->dfa.sparse_kernel == PM_SK_PRODUCT || o->dfa.sparse_kernel == PM_SK_FL))
+        ap.queue[ap.nq++] = CAND_SPARSE16;
     ap.qi = 0;
     ap.trial = 0;
 }

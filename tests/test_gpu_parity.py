@@ -706,7 +706,7 @@ def test_full_size_merged_deep_auto_oracle_windows(stream):
         torch.cuda.synchronize()
         held = au.hold_choice(0)
     held = au.hold_choice(2)
-    assert held in (1, 2, 3)
+    assert held in (1, 2, 3, 4)
     a.zero_()
     au.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c.data_ptr(), s)
     torch.cuda.synchronize()
@@ -1118,7 +1118,7 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
     m = matcher("et", "auto")
     kernels, forms = [], []
-    for _ in range(8):
+    for _ in range(10):
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
@@ -1126,11 +1126,11 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
         forms.append(m.dfa_form_last)
         assert torch.equal(got, want)
     # RT first (measured: it spills), then two trial launches of each DFA
-    # form (dense rows, then rows + records; the second of each timed); the
-    # fastest of the three per position holds after that
-    assert kernels[:5] == [pm.KIND_RT] + [pm.KIND_AC] * 4, kernels
-    assert forms[:5] == [0, 1, 1, 2, 2], forms
-    assert len(set(zip(kernels[5:], forms[5:]))) == 1, (kernels, forms)
+    # candidate (dense rows; rows + records; the same with 16-B record
+    # loads; the second of each timed); the fastest per position holds
+    assert kernels[:7] == [pm.KIND_RT] + [pm.KIND_AC] * 6, kernels
+    assert forms[:7] == [0, 1, 1, 2, 2, 2, 2], forms
+    assert len(set(zip(kernels[7:], forms[7:]))) == 1, (kernels, forms)
 
 
 @pytest.mark.parametrize("cap", [1, 2])
@@ -1225,7 +1225,7 @@ def test_auto_scan_device_across_two_streams_and_hold():
         torch.cuda.synchronize()
         assert torch.equal(o, want)
         held = m.hold_choice(0)
-    assert held in (1, 2, 3), held
+    assert held in (1, 2, 3, 4), held
     assert m.hold_choice(100) == held  # pinned for the next 100 launches
     for _ in range(3):
         m.scan_device(dt.data_ptr(), 0, 0, n, outs[1].data_ptr(), None, streams[1].cuda_stream)
@@ -1343,8 +1343,9 @@ def test_spill_cap_raised_after_prepare():
 
 @pytest.mark.parametrize("stream", ["ship", "lines"])
 def test_ac_kind_times_both_dfa_forms(stream):
-    """The AC kind tries its two forms (two launches each, the second timed)
-    and holds the faster; every launch equals the RT kernel."""
+    """The AC kind tries its forms (dense rows, rows + records, the latter
+    also with every record loaded as a 16-B half; two launches each, the
+    second timed) and holds the fastest; every launch equals the RT kernel."""
     import torch
     n = 16 << 20
     s = torch.cuda.current_stream()
@@ -1357,14 +1358,16 @@ def test_ac_kind_times_both_dfa_forms(stream):
     want = torch.empty(n, dtype=torch.int32, device="cuda")
     rt.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
     forms = []
-    for _ in range(7):
+    for _ in range(9):
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
         assert ac.kernel_last == pm.KIND_AC
         forms.append(ac.dfa_form_last)
         assert torch.equal(got, want)
-    assert forms[:4] == [1, 1, 2, 2] and forms[4] == forms[5] == forms[6] in (1, 2), forms
+    # dense rows, rows + records, the same with 16-B record loads: two
+    # launches each, then the fastest holds
+    assert forms[:6] == [1, 1, 2, 2, 2, 2] and forms[6] == forms[7] == forms[8] in (1, 2), forms
     ac.reset()  # a new stream: the forms are timed again
     ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
     torch.cuda.synchronize()
