@@ -538,6 +538,7 @@ def main():
         d_matches = all_reduce(dcnt.clone(), dist.ReduceOp.SUM).item() // dsteps
         ach = n * 5 / (d_ms * 1e-3) / 1e9
         dtr = load_traffic(f"{args.dict}-lines-{n}-dense-auto")
+        d_gather = gather_roofline(lib, ma, d_ms, dtr)
         deep = {"kernel": "auto kind (RT, or after a deep RT launch the faster AC-DFA form by timed trials)",
                 "picked": CAND_NAME.get(d_held, str(d_held)), "stream": "lines", "mode": "dense",
                 "steps": dsteps, "kernel_ms": round(d_ms, 4),
@@ -549,6 +550,7 @@ def main():
                              "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": n * 5,
                              "traffic": dtr["traffic_bytes"] if dtr else None,
                              "traffic_source": dtr["source"] if dtr else None},
+                "gather_roofline": d_gather,
                 "cpu_baseline": cpu.get("deep") if cpu else None}
         ma.free()
         del ma
@@ -700,6 +702,8 @@ def other_configs(args, pm, lib, world, all_reduce, dist, text, out):
                                   "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes * 5,
                                   "traffic": tr["traffic_bytes"] if tr else None,
                                   "traffic_source": tr["source"] if tr else None}}
+        if kind != "rt":
+            res[name]["gather_roofline"] = gather_roofline(lib, m, ms, tr)
         m.free()
         del t, o
 
@@ -708,6 +712,41 @@ def other_configs(args, pm, lib, world, all_reduce, dist, text, out):
     run("merged_lines_auto", "merged", "auto", "lines", min(args.bytes, 1 << 30), 5)
     run("merged_ship_auto", "merged", "auto", "ship", min(args.bytes, 1 << 30), 5)
     return res
+
+
+def gather_roofline(lib, mat, kernel_ms, tr, steps=2048):
+    """The DFA kernels' own bound: table gathers, not HBM bytes.  The ceiling
+    is measured live, pm_hip_gather_ceiling_device over the object's own
+    sparse image (the deep kernel's 1,024 lanes per CU, each chasing
+    dependent 4-B loads at uniform indices; median of 3 timed launches);
+    achieved = the L2 read requests of one launch (rocprofv3
+    TCP_TCC_READ_REQ_sum from profiles/traffic.json: table loads and text)
+    / the kernel time.  None without the image or the PMC entry."""
+    import torch
+    s = torch.cuda.current_stream()
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    ts = []
+    for r in range(4):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        rc = lib.pm_hip_gather_ceiling_device(mat.obj, steps, sink.data_ptr(), s.cuda_stream)
+        e1.record(s)
+        torch.cuda.synchronize()
+        if rc != 0:
+            return None
+        if r:
+            ts.append(e0.elapsed_time(e1))
+    ms = sorted(ts)[len(ts) // 2]
+    ceiling = steps * 1024 * ncu / (ms * 1e-3) / 1e9
+    req = tr.get("l2_read_requests") if tr else None
+    ach = req / (kernel_ms * 1e-3) / 1e9 if req else None
+    return {"bound": "gathers", "unit": "G loads/s", "ceiling": round(ceiling, 2),
+            "achieved": round(ach, 2) if ach else None, "frac": round(ach / ceiling, 4) if ach else None,
+            "requests_per_launch": req, "ceiling_ms": round(ms, 4), "ceiling_loads": steps * 1024 * ncu,
+            "what": "ceiling: pm_hip_gather_ceiling_device over this object's FL image (dependent uniform 4-B "
+                    "loads, the kernel's launch shape); achieved: TCP_TCC_READ_REQ_sum per launch "
+                    "(profiles/traffic.json) / kernel time"}
 
 
 def load_traffic(workload_key):

@@ -224,6 +224,14 @@ int pm_hip_set_option(void* obj, const char* name, int64_t value);
  * ids) over d_text[0, n).  bench.py's live floor.  0 on success. */
 int pm_hip_streaming_floor_device(void* obj, const uint8_t* d_text, int64_t n, void* d_out, int out_width,
                                   void* hip_stream);
+/* The gather ceiling of the object's sparse DFA image (the fallback-linked
+ * form; ac / auto kinds): one 1,024-lane workgroup per CU, each lane making
+ * `steps` dependent 4-B loads at hashed, uniform indices over the image --
+ * the deep kernel's loads without its logic, over its own table.  bench.py
+ * times it beside the DFA legs: steps * 1,024 * CUs loads per launch.
+ * d_sink: one device u32 (not written in practice).  0, -2 without the
+ * image, -3 on a launch error. */
+int pm_hip_gather_ceiling_device(void* obj, int steps, uint32_t* d_sink, void* hip_stream);
 /* The read_block host path's breakdown since the last call -- out5 =
  * {staging s, enqueue s, wait s, result copy / map s, calls} -- then reset
  * and turn the accounting on (on != 0) or off.  Process-wide accounting;

@@ -111,6 +111,7 @@ SIGNATURES = {
     "pm_hip_set_device": (ctypes.c_int, [ctypes.c_int]),
     "pm_hip_set_option": (ctypes.c_int, [c_vp, ctypes.c_char_p, ctypes.c_int64]),
     "pm_hip_streaming_floor_device": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, c_vp, ctypes.c_int, c_vp]),
+    "pm_hip_gather_ceiling_device": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp]),
     "pm_hip_sparse_kernel_last": (ctypes.c_int, [c_vp]),
     # host-only table images
     "pm_flat_build": (c_vp, [ctypes.POINTER(ctypes.c_char_p), c_u32p, ctypes.c_size_t, ctypes.c_int]),

@@ -74,6 +74,7 @@ struct DfaDev {
     const uint16_t* flrowout16;
     uint32_t flF;
     uint32_t flGD;  // first deep granule (pm_flatten.h FlImage::deep_g)
+    uint32_t flwords;  // 4-B words of the FL image (rows, then records)
 };
 
 // Positions [pos0, pos0+n) of text; bytes back to stream_start are context.
@@ -85,6 +86,12 @@ hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0,
 // and stores, no lookups; its ids are not matches) over text[0, n).
 hipError_t pm_launch_rt_floor(const uint8_t* text, int64_t n, void* out, int outw, const RtDev& t, int num_cu,
                               hipStream_t s);
+// The gather ceiling of a table of `words` 4-B words (bench.py's live bound
+// for the DFA legs): the sparse kernel's launch shape (1,024 lanes per CU),
+// each lane chasing `steps` dependent 4-B loads at hashed indices; *sink is
+// never written in practice.
+hipError_t pm_launch_gather_probe(const uint32_t* table, uint32_t words, int steps, uint32_t* sink, int num_cu,
+                                  hipStream_t s);
 // The DFA form DfaDev::form names (0: the sparse one when the automaton has
 // it), and for the sparse form DfaDev::sparse_kernel (0: the product choice).
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,

@@ -2116,6 +2116,17 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
     }
 }
 
+// The gather ceiling (pm_launch_gather_probe): the FL kernel's lanes
+// without its logic -- each lane's next index is a hash of the word it
+// loaded, so the loads are dependent and uniform over the table.
+__global__ __launch_bounds__(1024) void gather_probe_kernel(const uint32_t* __restrict__ tab, uint32_t words,
+                                                            int steps, uint32_t* __restrict__ sink) {
+    const uint32_t lane = blockIdx.x * 1024u + threadIdx.x;
+    uint32_t idx = __umulhi(lane * 0x9E3779B1u, words);
+    for (int j = 0; j < steps; ++j) idx = __umulhi((tab[idx] ^ (lane + (uint32_t)j)) * 0x9E3779B1u, words);
+    if (idx == 0xFFFFFFFFu) sink[0] = idx;  // (idx < words: never; keeps the chain)
+}
+
 // Accuracy of one id stream against a reference one (Core/src/measure.c:
 // 174-190 with is_pattern_suffix, PatternsTree.c:485-494), one position per
 // lane-element: equal -> success; algo on real's parent chain -> partial;
@@ -2290,6 +2301,13 @@ static int64_t rt_spill_stride(int64_t n, int64_t blocks, int64_t wave_cap) {
     const int64_t nw = blocks * RT_WAVES;
     const int64_t natural = ((n / RT_CHUNK + nw - 1) / nw) * RT_CHUNK;
     return natural < wave_cap ? natural : wave_cap;
+}
+
+hipError_t pm_launch_gather_probe(const uint32_t* table, uint32_t words, int steps, uint32_t* sink, int num_cu,
+                                  hipStream_t s) {
+    if (!table || words == 0 || steps <= 0 || num_cu <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gather_probe_kernel, dim3((unsigned)num_cu), dim3(1024), 0, s, table, words, steps, sink);
+    return hipGetLastError();
 }
 
 int64_t pm_rt_spill_items(int64_t n, int num_cu, int64_t cap_chunks) {

@@ -929,6 +929,7 @@ void pm_hip_compile(void* obj) {
                 o->dfa.flrowout16 = (const uint16_t*)dalloc_copy(o, fl.rowout16.data(), fl.rowout16.size() * 2);
                 o->dfa.flF = fl.F;
                 o->dfa.flGD = fl.deep_g;
+                o->dfa.flwords = (uint32_t)(fl.block.size() - 16);
             }
         }
     }
@@ -1194,6 +1195,20 @@ int pm_hip_streaming_floor_device(void* obj, const uint8_t* d_text, int64_t n, v
     t.spill_cap = o->spill_cap;
     hipError_t e = pm_launch_rt_floor(d_text, n, d_out, out_width, t, o->num_cu, (hipStream_t)hip_stream);
     return e == hipSuccess ? 0 : -3;
+}
+
+int pm_hip_gather_ceiling_device(void* obj, int steps, uint32_t* d_sink, void* hip_stream) {
+    PmHip* o = as(obj);
+    if (!o->compiled || !o->dfa.flbase) return -2;
+    hipError_t e = hipSetDevice(o->device);
+    if (e == hipSuccess)
+        e = pm_launch_gather_probe(reinterpret_cast<const uint32_t*>(o->dfa.flbase), o->dfa.flwords, steps, d_sink,
+                                   o->num_cu, (hipStream_t)hip_stream);
+    if (e != hipSuccess) {
+        std::snprintf(g_err, sizeof(g_err), "gather_ceiling: %s", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
 }
 
 int pm_hip_set_option(void* obj, const char* name, int64_t value) {

@@ -2,7 +2,8 @@
 """Summarise a gpu_round5.sh session directory: per leg, the dominant scan
 kernel's rocprofv3 average duration (--stats) and its PMC traffic per
 bench step (FETCH_SIZE / WRITE_SIZE medians over its dispatches x the
-dispatches one step makes).  Writes <dir>/legs.json; with --traffic FILE
+dispatches one step makes; for the DFA legs also TCP_TCC_READ_REQ_sum, the
+L2 read requests bench.py sets against its live gather ceiling).  Writes <dir>/legs.json; with --traffic FILE
 also merges the legs into profiles/traffic.json's format (FILE), citing
 --cite (the directory the session is committed under)."""
 import argparse
@@ -69,6 +70,8 @@ def main():
             n = int(key.split("-")[2])
             ent.update({"read_bytes_raw": raw, "read_bytes_corrected": rd, "write_bytes": wr,
                         "traffic_bytes": rd + wr, "algorithmic_bytes": n * ALG[mode]})
+        if "TCP_TCC_READ_REQ_sum" in med:  # L2 read requests (the DFA kernels' gathers + text)
+            ent["l2_read_requests"] = med["TCP_TCC_READ_REQ_sum"] * per_step
         legs[leg] = ent
     json.dump(legs, open(os.path.join(a.dir, "legs.json"), "w"), indent=1)
     for leg, e in legs.items():
@@ -85,6 +88,7 @@ def main():
                 "read_bytes_raw": e["read_bytes_raw"], "read_bytes_corrected": e["read_bytes_corrected"],
                 "write_bytes": e["write_bytes"], "traffic_bytes": e["traffic_bytes"],
                 "algorithmic_bytes": e["algorithmic_bytes"],
+                **({"l2_read_requests": e["l2_read_requests"]} if "l2_read_requests" in e else {}),
                 "note": "FETCH_SIZE (KiB) x1024 (x2 for the RT kernels' streaming text reads, MI355X_MICROARCH.md "
                         "§HBM; not for the DFA kernels' table gathers), WRITE_SIZE x1024; per bench step",
                 "session": os.path.basename(a.dir.rstrip("/"))}

@@ -3,7 +3,8 @@
 # for every leg of that line (headline C3, count only, deep, and each
 # `configs` entry) one rocprofv3 --kernel-trace --stats run of the
 # equivalent single-workload bench command plus the two PMC traffic passes
-# (FETCH_SIZE, WRITE_SIZE: one counter per pass, --kernel-trace only).
+# (FETCH_SIZE, WRITE_SIZE; for the DFA legs TCP_TCC_READ_REQ_sum too: one
+# counter per pass, --kernel-trace only).
 # Usage: gpu_round5.sh TAG [legs...]   (legs default: all; "tests" / "bench"
 # / a leg name).  Every GPU step has its own time limit; the first failure
 # ends the script.
@@ -41,7 +42,9 @@ for leg in c3 count deep c2 c5 merged_lines merged_ship; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$leg" -o bench -- \
       python3 "$ROOT/bench.py" --no-cpu --no-extra $a > "$OUT/bench_prof_$leg.json" 2> "$OUT/bench_prof_$leg.err" \
       || { tail "$OUT/bench_prof_$leg.err"; exit 1; }
-  for c in FETCH_SIZE WRITE_SIZE; do
+  CTRS="FETCH_SIZE WRITE_SIZE"
+  case $leg in deep|merged_lines|merged_ship) CTRS="$CTRS TCP_TCC_READ_REQ_sum";; esac
+  for c in $CTRS; do
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d "$OUT/pmc_$leg/$c" -o c -- \
         python3 "$ROOT/bench.py" --no-cpu --no-extra ${a/--steps [0-9]*/--steps 3} --warmup 1 > "$OUT/pmc_${leg}_$c.log" 2>&1 \
         || { tail "$OUT/pmc_${leg}_$c.log"; exit 1; }

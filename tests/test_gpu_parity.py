@@ -894,6 +894,20 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
 SPARSE_KERNELS = {1: (4, 2, 0), 2: (4,), 3: (4, 2), 4: (4, 2, 0), 5: (4, 2, 0)}
 
 
+def test_gather_ceiling_probe():
+    """pm_hip_gather_ceiling_device (bench.py's live bound for the DFA legs):
+    runs over an ac object's own FL image and finishes; an rt object, which
+    has no such image, gets -2 and launches nothing."""
+    torch = _torch()
+    lib = pm.load()
+    s = torch.cuda.current_stream()
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    assert lib.pm_hip_gather_ceiling_device(matcher("snort", "ac").obj, 64, sink.data_ptr(), s.cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert int(sink.item()) == 0
+    assert lib.pm_hip_gather_ceiling_device(matcher("snort", "rt").obj, 64, sink.data_ptr(), s.cuda_stream) == -2
+
+
 def test_sparse_form_without_8b_units():
     """An automaton inside the coded range whose 8-B record units do not fit
     the coded word (F + units > 2^20: 200,000 random 8-byte patterns over
