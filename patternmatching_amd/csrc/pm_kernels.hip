@@ -1963,12 +1963,15 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
 // (the state it starts from holds it).  OUTW 4 / 2: u32 / u16 ids (a u16
 // block of a chain is 64 B: four lanes' 16-B stores, 16 chains per store
 // instruction); 0: the count alone, no staging rows, no escapes, no stores.
-template <int KR, int OUTW = 4>
+// H16: every record held as a 16-B half (the picks' CAND_SPARSE16 trial;
+// its own instance, so profiles tell it from the product's launches).
+template <int KR, int OUTW = 4, bool H16 = false>
 __global__ __launch_bounds__(1024) void dfa_fl_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
     const uint16_t* __restrict__ rowout16, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
     static_assert(OUTW == 0 || OUTW == 2 || OUTW == 4, "u32 / u16 ids or the count");
+    if (H16) GD = 0xFFFFFFFFu;
     constexpr int THREADS = 1024, BLK = 32, SROW = 17;
     constexpr bool kIds = OUTW != 0;
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
@@ -2122,9 +2125,13 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
 __global__ __launch_bounds__(1024) void gather_probe_kernel(const uint32_t* __restrict__ tab, uint32_t words,
                                                             int steps, uint32_t* __restrict__ sink) {
     const uint32_t lane = blockIdx.x * 1024u + threadIdx.x;
-    uint32_t idx = __umulhi(lane * 0x9E3779B1u, words);
-    for (int j = 0; j < steps; ++j) idx = __umulhi((tab[idx] ^ (lane + (uint32_t)j)) * 0x9E3779B1u, words);
-    if (idx == 0xFFFFFFFFu) sink[0] = idx;  // (idx < words: never; keeps the chain)
+    uint32_t idx = __umulhi(lane * 0x9E3779B1u, words), acc = 0;
+    for (int j = 0; j < steps; ++j) {
+        const uint32_t v = tab[idx];
+        acc += v;
+        idx = __umulhi((v ^ (lane + (uint32_t)j)) * 0x9E3779B1u, words);
+    }
+    if (acc == 0x9E3779B1u && idx == 1u) sink[0] = acc;  // (all but never; keeps the chain live)
 }
 
 // Accuracy of one id stream against a reference one (Core/src/measure.c:
@@ -2461,15 +2468,19 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         const dim3 gs((unsigned)wg), bs(wgt);
         switch (sk) {
             case PM_SK_FL:
-                if (outw == 4)
-                    hipLaunchKernelGGL((dfa_fl_kernel<FL_LDS_ROWS, 4>), gs, bs, 0, s, text, stream_start, pos0, n, out,
-                                       count, t.flbase, t.flF, t.flGD, t.flrowout16, t.warm, seg, g3);
-                else if (outw == 2)
-                    hipLaunchKernelGGL((dfa_fl_kernel<FL_LDS_ROWS, 2>), gs, bs, 0, s, text, stream_start, pos0, n, out,
-                                       count, t.flbase, t.flF, t.flGD, t.flrowout16, t.warm, seg, g3);
-                else
-                    hipLaunchKernelGGL((dfa_fl_kernel<FL_COUNT_LDS_ROWS, 0>), gs, bs, 0, s, text, stream_start, pos0,
-                                       n, out, count, t.flbase, t.flF, t.flGD, t.flrowout16, t.warm, seg, g3);
+#define PM_FL_LAUNCH(KR_, W_, H_)                                                                                  \
+    hipLaunchKernelGGL((dfa_fl_kernel<KR_, W_, H_>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, t.flbase, \
+                       t.flF, t.flGD, t.flrowout16, t.warm, seg, g3)
+                if (t.flGD == 0xFFFFFFFFu) {  // every record as a 16-B half
+                    if (outw == 4) PM_FL_LAUNCH(FL_LDS_ROWS, 4, true);
+                    else if (outw == 2) PM_FL_LAUNCH(FL_LDS_ROWS, 2, true);
+                    else PM_FL_LAUNCH(FL_COUNT_LDS_ROWS, 0, true);
+                } else {
+                    if (outw == 4) PM_FL_LAUNCH(FL_LDS_ROWS, 4, false);
+                    else if (outw == 2) PM_FL_LAUNCH(FL_LDS_ROWS, 2, false);
+                    else PM_FL_LAUNCH(FL_COUNT_LDS_ROWS, 0, false);
+                }
+#undef PM_FL_LAUNCH
                 break;
             case PM_SK_STAGE16:
                 hipLaunchKernelGGL((dfa_sparse_stage16_kernel<88, 4, true>), gs, bs, 0, s, text, stream_start, pos0, n,
