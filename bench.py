@@ -746,7 +746,8 @@ def gather_roofline(lib, mat, kernel_ms, tr, steps=2048):
             "requests_per_launch": req, "ceiling_ms": round(ms, 4), "ceiling_loads": steps * 1024 * ncu,
             "what": "ceiling: pm_hip_gather_ceiling_device over this object's FL image (dependent uniform 4-B "
                     "loads, the kernel's launch shape); achieved: TCP_TCC_READ_REQ_sum per launch "
-                    "(profiles/traffic.json) / kernel time"}
+                    "(profiles/traffic.json: the L2 read requests, the table loads and ~1/16 per byte of text "
+                    "loads) / kernel time"}
 
 
 def load_traffic(workload_key):
