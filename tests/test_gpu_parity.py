@@ -894,6 +894,44 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
 SPARSE_KERNELS = {1: (4, 2, 0), 2: (4,), 3: (4, 2), 4: (4, 2, 0), 5: (4, 2, 0)}
 
 
+@pytest.mark.parametrize("key", ["et", "merged"])
+def test_fl_kernel_every_width(key):
+    """The fallback-linked kernel (sparse_kernel 1) on et and the merged
+    dictionaries, 8 MiB of each one's lines stream plus the shipped stream:
+    u32 ids, u16 ids and the count equal the reverse-trie kernel's."""
+    torch = _torch()
+    rt, ac = matcher(key, "rt"), matcher(key, "ac")
+    n = 8 << 20
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    try:
+        assert ac.set_option("dfa_form", 2) == 0 and ac.set_option("sparse_kernel", 1) == 0
+        for stream in ("lines", "ship"):
+            if stream == "lines":
+                rt.gen_lines_device(dt.data_ptr(), n + 64, 21, s)
+            else:
+                dt.copy_(torch.from_numpy(np.tile(SHIP, (n + 64) // len(SHIP) + 1)[: n + 64]).cuda())
+            ref = torch.empty(n, dtype=torch.int32, device="cuda")
+            rt.scan_device(dt.data_ptr(), 0, 0, n, ref.data_ptr(), None, s)
+            a = torch.zeros(n, dtype=torch.int32, device="cuda")
+            h = torch.zeros(n, dtype=torch.int16, device="cuda")
+            c = torch.zeros(2, dtype=torch.int64, device="cuda")
+            ac.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c[0:1].data_ptr(), s)
+            assert ac.sparse_kernel_last == 1
+            ac.scan_device(dt.data_ptr(), 0, 0, n, h.data_ptr(), None, s, out_width=2)
+            assert ac.sparse_kernel_last == 1
+            ac.scan_device(dt.data_ptr(), 0, 0, n, 0, c[1:2].data_ptr(), s)
+            assert ac.sparse_kernel_last == 1
+            torch.cuda.synchronize()
+            assert torch.equal(a, ref), stream
+            assert torch.equal(h.to(torch.int32) & 0xFFFF, ref), stream
+            nz = int((ref != 0).sum().item())
+            assert int(c[0].item()) == nz and int(c[1].item()) == nz, stream
+    finally:
+        ac.set_option("sparse_kernel", 0)
+        ac.set_option("dfa_form", 0)
+
+
 def test_gather_ceiling_probe():
     """pm_hip_gather_ceiling_device (bench.py's live bound for the DFA legs):
     runs over an ac object's own FL image and finishes; an rt object, which
