@@ -588,7 +588,7 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
     uint64_t u = 0;
     for (int part = 0; part < 2; ++part) {
         if (part == 1) {
-            u = (u + 3) & ~(uint64_t)3;  // the deep part starts a 32-B block
+            u = (u + 7) & ~(uint64_t)7;  // the deep part starts a 64-B block (the kernel's: 32 or 64 B)
             fl.deep_g = (uint32_t)u;
         }
         for (uint32_t v = F; v < S; ++v) {

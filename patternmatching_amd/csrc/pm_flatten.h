@@ -201,7 +201,7 @@ constexpr uint32_t PM_FL_FB_INREC = 4095;  // the 12-bit field's top value
 constexpr uint32_t PM_FL_LDS_ROWS = 88;  // rows the kernel stages in LDS (dfa_fl_kernel<88>)
 // Records of trie depth < PM_FL_DEEP_DEPTH come first (the kernel loads
 // them as 16-B halves: a walk rarely stays), then, from granule deep_g (a
-// multiple of 4), the deeper ones (loaded as aligned 32-B blocks: a walk
+// multiple of 8), the deeper ones (loaded as aligned 32-B blocks: a walk
 // that got this deep is usually on a pattern's unary run, whose records
 // follow each other).  Within each part, the trie's order.
 #ifndef PM_FL_DEEP_DEPTH

@@ -1882,19 +1882,49 @@ static_assert(PM_FL_SPEC == 0 || PM_FL_SPEC == 2, "PM_FL_SPEC: 0 (product) or 2 
 // below GD, pm_flatten.h FlImage::deep_g) the 16-B half holding it, in R0;
 // for a deep one the aligned 32-B block, R0 and R1.  The held key: the
 // half's index, or the block's with the top bit set.
-__device__ __forceinline__ uint32_t fl_key(uint32_t g, bool deep) { return deep ? (g >> 2) | 0x80000000u : g >> 1; }
+// The deep records' block: PM_FL_DEEP_BLK bytes (32, the product, or 64 --
+// an ablation build), NR 16-B registers.
+#ifndef PM_FL_DEEP_BLK
+#define PM_FL_DEEP_BLK 32
+#endif
+static_assert(PM_FL_DEEP_BLK == 32 || PM_FL_DEEP_BLK == 64, "PM_FL_DEEP_BLK: 32 or 64");
+constexpr int FL_NR = PM_FL_DEEP_BLK / 16;
+constexpr uint32_t FL_DSHIFT = PM_FL_DEEP_BLK == 64 ? 3u : 2u;  // granules per deep block: 4 or 8
+struct FlHold {
+    tu32x4 R[FL_NR];
+};
+
+__device__ __forceinline__ uint32_t fl_key(uint32_t g, bool deep) {
+    return deep ? (g >> FL_DSHIFT) | 0x80000000u : g >> 1;
+}
 
 __device__ __forceinline__ void fl_load(const uint8_t* __restrict__ base, uint32_t F, uint32_t g, bool deep,
-                                        tu32x4& R0, tu32x4& R1) {
-    const tu32x4* p = reinterpret_cast<const tu32x4*>(base + F * 1024u + ((g >> 1) & (deep ? ~1u : ~0u)) * 16u);
-    R0 = p[0];
-    if (deep) R1 = p[1];
+                                        FlHold& H) {
+    const tu32x4* p =
+        reinterpret_cast<const tu32x4*>(base + F * 1024u + ((g >> 1) & (deep ? ~(uint32_t)(FL_NR - 1) : ~0u)) * 16u);
+    H.R[0] = p[0];
+    if (deep) {
+#pragma unroll
+        for (int k = 1; k < FL_NR; ++k) H.R[k] = p[k];
+    }
+}
+
+__device__ __forceinline__ tu32x4 bsel4(uint32_t m, const tu32x4& a, const tu32x4& b) {
+    return tu32x4{bsel(m, a.x, b.x), bsel(m, a.y, b.y), bsel(m, a.z, b.z), bsel(m, a.w, b.w)};
+}
+
+// The 16-B register holding granule g (a shallow half is always R[0]).
+__device__ __forceinline__ tu32x4 fl_reg(const FlHold& H, uint32_t g, bool deep) {
+    const uint32_t m2 = bmask(deep && (g & 2u));
+    if (FL_NR == 2) return bsel4(m2, H.R[0], H.R[FL_NR - 1]);
+    const uint32_t m4 = bmask(deep && (g & 4u));
+    return bsel4(m4, bsel4(m2, H.R[0], H.R[1 % FL_NR]), bsel4(m2, H.R[2 % FL_NR], H.R[3 % FL_NR]));
 }
 
 template <int KR>
 __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
                                             const uint32_t* __restrict__ s_rows, uint32_t w, uint32_t c,
-                                            uint32_t& cb, tu32x4& R0, tu32x4& R1, uint32_t& own) {
+                                            uint32_t& cb, FlHold& H, uint32_t& own) {
     const uint32_t s = w & DFA_STATE_MASK;
     const bool isrow = s < F;
     const uint32_t g = s - F;
@@ -1909,17 +1939,15 @@ __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, ui
     uint32_t x = 0;
     if ((isrow && !lrow) || pre) x = *reinterpret_cast<const uint32_t*>(base + (bsel(bmask(isrow), fb, s) * 1024u + c * 4u));
     if (newblk) {
-        fl_load(base, F, g, deep, R0, R1);
+        fl_load(base, F, g, deep, H);
         cb = key;
     }
     const uint32_t lw = s_rows[(bmask(lrow) & s) * 256u + c];  // (row 0 for the other lanes: no branch)
     // words 2e .. 2e + 3 of what the lane holds, e the granule in it (a
     // 16-B record starts at an even granule)
-    const uint32_t m1 = bmask(g & 1u), m2 = bmask(deep && (g & 2u));
-    const uint32_t w0 = bsel(m2, bsel(m1, R0.x, R0.z), bsel(m1, R1.x, R1.z));
-    const uint32_t w1 = bsel(m2, bsel(m1, R0.y, R0.w), bsel(m1, R1.y, R1.w));
-    const uint32_t w2 = bsel(m2, R0.z, R1.z);
-    const uint32_t w3 = bsel(m2, R0.w, R1.w);
+    const tu32x4 RR = fl_reg(H, g, deep);
+    const uint32_t m1 = bmask(g & 1u);
+    const uint32_t w0 = bsel(m1, RR.x, RR.z), w1 = bsel(m1, RR.y, RR.w), w2 = RR.z, w3 = RR.w;
     own = w0 & 0xFFFFu;
     const bool h0 = c == ((w0 >> 16) & 0xFFu), h1 = c == (w0 >> 24);
     const uint32_t row = bsel(bmask(fb == PM_FL_INREC), fb, w3);
@@ -1934,11 +1962,11 @@ __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, ui
 }
 
 // The output of the position that produced w: a record's own out16 (what
-// holds it loaded into R0 / R1 if the lane does not hold it -- the next
-// step's load, made early), or a row word's code; *esc = the code escapes
-// (the answer is then rowout16[w & MASK]).
+// holds it loaded if the lane does not hold it -- the next step's load,
+// made early), or a row word's code; *esc = the code escapes (the answer
+// is then rowout16[w & MASK]).
 __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, uint32_t F, uint32_t GD, uint32_t w,
-                                              uint32_t& cb, tu32x4& R0, tu32x4& R1, bool& esc) {
+                                              uint32_t& cb, FlHold& H, bool& esc) {
     const uint32_t s = w & DFA_STATE_MASK;
     esc = false;
     if (s < F) {
@@ -1949,11 +1977,11 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
     const bool deep = g >= GD;
     const uint32_t key = fl_key(g, deep);
     if (key != cb) {
-        fl_load(base, F, g, deep, R0, R1);
+        fl_load(base, F, g, deep, H);
         cb = key;
     }
-    const uint32_t w0 = (deep && (g & 2u)) ? ((g & 1u) ? R1.z : R1.x) : ((g & 1u) ? R0.z : R0.x);
-    return w0 & 0xFFFFu;
+    const tu32x4 RR = fl_reg(H, g, deep);
+    return ((g & 1u) ? RR.z : RR.x) & 0xFFFFu;
 }
 
 // The FL form's scan: the staged-id structure of dfa_sparse_stage16_kernel
@@ -1989,7 +2017,9 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
     const int64_t nseg = (n + seg_len - 1) / seg_len;
     const int64_t lanes = (int64_t)gridDim.x * THREADS;
     uint32_t cnt = 0, cb = 0xFFFFFFFFu, own = 0;
-    tu32x4 R0 = {0u, 0u, 0u, 0u}, R1 = {0u, 0u, 0u, 0u};
+    FlHold H;
+#pragma unroll
+    for (int k = 0; k < FL_NR; ++k) H.R[k] = tu32x4{0u, 0u, 0u, 0u};
     for (int64_t sg0 = (int64_t)blockIdx.x * THREADS + threadIdx.x; __ballot(sg0 < nseg); sg0 += lanes) {
         const bool has = sg0 < nseg;
         // the wave's segments are consecutive: a wave-uniform 64-bit base
@@ -2003,7 +2033,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
         int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
         if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
         uint32_t w = 0;  // the root, reached by no word
-        for (int64_t i = wlo; i < lo; ++i) w = fl_step<KR>(base, F, GD, s_rows, w, text[i], cb, R0, R1, own);
+        for (int64_t i = wlo; i < lo; ++i) w = fl_step<KR>(base, F, GD, s_rows, w, text[i], cb, H, own);
         const int64_t nblk = seg_len / BLK;
         for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
             bool act[2];
@@ -2031,7 +2061,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
 #pragma unroll
                 for (int j = 0; j < BLK; ++j) {
                     const uint32_t wn = fl_step<KR>(base, F, GD, s_rows, w, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb,
-                                                    R0, R1, own);
+                                                    H, own);
                     if (j > 0) {  // the output of position j - 1, which produced w
                         const bool rec = (w & DFA_STATE_MASK) >= F;
                         const uint32_t code = w >> 20;
@@ -2047,7 +2077,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 }
                 {  // position 31
                     bool esc;
-                    const uint32_t id = fl_output(base, F, GD, w, cb, R0, R1, esc);
+                    const uint32_t id = fl_output(base, F, GD, w, cb, H, esc);
                     if (kIds) {
                         my[BLK - 1] = (uint16_t)(esc ? (w & DFA_STATE_MASK) : id);
                         em |= esc ? 1u << (BLK - 1) : 0u;
@@ -2104,9 +2134,9 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
         }
         // the segment's last (< BLK) positions
         for (int64_t i = lo + BLK * ((hi - lo) / BLK); i < hi; ++i) {
-            w = fl_step<KR>(base, F, GD, s_rows, w, text[i], cb, R0, R1, own);
+            w = fl_step<KR>(base, F, GD, s_rows, w, text[i], cb, H, own);
             bool esc;
-            uint32_t id = fl_output(base, F, GD, w, cb, R0, R1, esc);
+            uint32_t id = fl_output(base, F, GD, w, cb, H, esc);
             if (kIds && esc) id = rowout16[w & DFA_STATE_MASK];
             if (OUTW == 4) reinterpret_cast<uint32_t*>(out)[i - pos0] = id;
             if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[i - pos0] = (uint16_t)id;

@@ -122,7 +122,7 @@ int main(int argc, char** argv) {
         roff[fl.granules] = off;
         printf("compact chains: records %.2f MB -> %.2f MB\n", fl.granules * 8 / 1e6, off / 1e6);
     }
-    for (int layout = 0; layout < 3; ++layout) {
+    for (int layout = 0; layout < 5; ++layout) {
         Lru l2{(size_t)L2KB * 1024 / 128};
         uint64_t rowreq = 0, recreq = 0, fbreq = 0, steps = 0, rowmiss = 0, recmiss = 0, fbmiss = 0;
         std::unordered_map<uint64_t, uint64_t> lines;
@@ -145,7 +145,8 @@ int main(int argc, char** argv) {
                 } else {
                     const uint32_t gr = s - F;
                     const bool deep = gr >= fl.deep_g;
-                    const uint32_t k = deep ? (gr >> 2) | 0x80000000u : gr >> 1;
+                    // layouts 3 / 4: deep records in 64-B / 128-B blocks
+                    const uint32_t k = deep ? (gr >> (layout == 3 ? 3 : layout == 4 ? 4 : 2)) | 0x80000000u : gr >> 1;
                     const uint64_t kk = layout == 2 ? roff[gr] / 32 : k;  // (layout 2: 32-B blocks by byte offset)
                     if (kk != key[L]) {
                         key[L] = (uint32_t)kk;
@@ -186,7 +187,7 @@ int main(int argc, char** argv) {
         }
         printf("%s: per step: row %.3f fallback %.3f record %.3f requests; L2 misses per step %.3f (row %.3f fb %.3f rec %.3f)\n"
                "   lines touched %zu (%.1f MB); 50/90/99%% of requests in %.2f / %.2f / %.2f MB\n",
-               layout == 2 ? "compact chains" : layout ? "permuted columns" : "product", (double)rowreq / steps, (double)fbreq / steps,
+               layout == 4 ? "deep 128-B blocks" : layout == 3 ? "deep 64-B blocks" : layout == 2 ? "compact chains" : layout ? "permuted columns" : "product", (double)rowreq / steps, (double)fbreq / steps,
                (double)recreq / steps, (double)(rowmiss + fbmiss + recmiss) / steps, (double)rowmiss / steps,
                (double)fbmiss / steps, (double)recmiss / steps, h.size(), h.size() * 128 / 1e6, n50 * 128 / 1e6,
                n90 * 128 / 1e6, n99 * 128 / 1e6);

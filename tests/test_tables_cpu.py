@@ -354,11 +354,11 @@ def test_fl_image_layout(key):
     two slots, or a fallback row past the word's 12-bit field (the word then
     holds 4095) -- starts at an even granule; the deep records start a
     32-B block; every word's record target is a granule inside the image,
-    and a row target is a row."""
+    and a row target is a row.  (deep_g: a 64-B boundary.)"""
     d, img, _ = image(key, pm.KIND_AC)
     F, granules, folded, deep_g = (int(v) for v in img.array("flinfo"))
     blk = img.array("flblock")
-    assert deep_g % 4 == 0 and deep_g <= granules and F > 0 and folded >= 0
+    assert deep_g % 8 == 0 and deep_g <= granules and F > 0 and folded >= 0
     assert len(blk) == F * 256 + 2 * granules
     rec = blk[F * 256:].reshape(-1, 2)
     rows = blk[:F * 256]
