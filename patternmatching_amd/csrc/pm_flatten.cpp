@@ -1,5 +1,6 @@
 // pm_flatten.cpp -- see pm_flatten.h.
 #include "pm_flatten.h"
+#include "pm_streamgen.h"
 
 #include <algorithm>
 #include <array>
@@ -537,7 +538,34 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
     return true;
 }
 
-bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
+std::vector<uint8_t> pm_fl_profile(const std::vector<std::string>& pats) {
+    std::vector<uint8_t> P;
+    std::vector<uint32_t> O(1, 0);
+    for (const std::string& p : pats) {
+        P.insert(P.end(), p.begin(), p.end());
+        O.push_back((uint32_t)P.size());
+    }
+    std::vector<uint8_t> t(PM_FL_PROFILE_PIECES * PM_FL_PROFILE_PIECE);
+    if (pats.empty()) return t;
+    std::vector<uint8_t> blk(PM_LINES_BLOCK);
+    for (size_t k = 0; k < PM_FL_PROFILE_PIECES; ++k) {
+        uint8_t* dst = t.data() + k * PM_FL_PROFILE_PIECE;
+        const uint64_t lo = (uint64_t)k << 30;  // far apart in either stream
+        for (uint64_t p = lo; p < lo + PM_FL_PROFILE_PIECE; ++p) {
+            if (k % 16 == 15) {
+                dst[p - lo] = pm_stream_byte(p, 7, 0);
+            } else {
+                if (p % PM_LINES_BLOCK == 0 || p == lo)
+                    pm_lines_block(blk.data(), PM_LINES_BLOCK, p / PM_LINES_BLOCK, P.data(), O.data(),
+                                   (uint32_t)pats.size(), 7);
+                dst[p - lo] = blk[p % PM_LINES_BLOCK];
+            }
+        }
+    }
+    return t;
+}
+
+bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl, const std::vector<uint8_t>* profile) {
     const uint32_t F = d.sF, S = d.states;
     fl = FlImage();
     if (d.sblock.empty() || F < 1 || F >= 65536) return false;
@@ -545,17 +573,42 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl) {
     auto R = [&](uint32_t v) { return rec + (size_t)(v - F) * 4; };  // {x, y, z, w} of record v
     for (uint32_t v = 0; v < S; ++v)
         if (d.sout[v] >= 65536) return false;
-    // rows: the first PM_FL_LDS_ROWS in the trie's breadth-first order (the
-    // root and the shallowest states: the rows the kernel stages in LDS, as
-    // the 8-B form does -- most row steps are theirs), then the others by
-    // fallback use, so the word's 12-bit field names the most used ones
-    // (scripts/sdfa_spec_model.cpp BFS88: lines stream 0.697 -> 0.662
-    // global requests per step, random ASCII 0.729 -> 0.699)
+    // rows: the first PM_FL_LDS_ROWS -- the rows the kernel stages in LDS
+    // -- are the root and the rows the profile's walks step from most
+    // (without a profile the trie's breadth-first order: the shallowest
+    // states), then the others by fallback use, so the word's 12-bit field
+    // names the most used ones
     std::vector<uint64_t> use(F, 0);
     for (uint32_t v = F; v < S; ++v) use[R(v)[3]]++;
     std::vector<uint32_t> ord(F), nrow(F);
     for (uint32_t r = 0; r < F; ++r) ord[r] = r;
     const uint32_t keep = std::min(F, PM_FL_LDS_ROWS);
+    if (profile && !profile->empty() && keep > 1) {
+        // the rows the profile's walks step from (row states, and record
+        // misses' fallback rows), one walk from the root per piece
+        std::vector<uint64_t> vis(F, 0);
+        const uint8_t* t = profile->data();
+        const size_t pieces = std::max<size_t>(1, profile->size() / PM_FL_PROFILE_PIECE);
+        for (size_t k = 0; k < pieces; ++k) {
+            const size_t lo = k * PM_FL_PROFILE_PIECE, hi = std::min(profile->size(), lo + PM_FL_PROFILE_PIECE);
+            uint32_t s = 0;
+            for (size_t i = lo; i < hi; ++i) {
+                const uint32_t c = t[i];
+                uint32_t row = s;
+                if (s >= F) {
+                    const uint32_t* r = R(s);
+                    if ((r[0] & 0x100u) && c == (r[0] & 0xFFu)) { s = r[1] & PM_DFA_STATE_MASK; continue; }
+                    if ((r[0] & 0x1000000u) && c == ((r[0] >> 16) & 0xFFu)) { s = r[2] & PM_DFA_STATE_MASK; continue; }
+                    row = r[3];
+                }
+                vis[row]++;
+                s = d.sblock[(size_t)row * 256 + c] & PM_DFA_STATE_MASK;
+            }
+        }
+        vis[0] = ~0ull;  // the root stays row 0 (the warm-ups' start)
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return vis[a] > vis[b]; });
+        std::sort(ord.begin() + keep, ord.end());  // (the rest: by fallback use, next)
+    }
     std::stable_sort(ord.begin() + keep, ord.end(), [&](uint32_t a, uint32_t b) { return use[a] > use[b]; });
     for (uint32_t k = 0; k < F; ++k) nrow[ord[k]] = k;
     // trie depth of every state, breadth first from the root: a row's

@@ -172,10 +172,11 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
 // lanes in lock step nearly every wave step waits for some lane's pair.
 // Here the word that leads INTO a record names its fallback row, so a
 // record needs no room for it and carries its own output instead.
-//   Rows [0, F): the first PM_FL_LDS_ROWS keep the trie's breadth-first
-//   order (the root and the shallowest states, staged in LDS by the
-//   kernel), the rest are renumbered by how many records fall back to
-//   them, so the fallback rows records use most have the smallest ids.
+//   Rows [0, F): the first PM_FL_LDS_ROWS are staged in LDS by the kernel
+//   (the root and, with a profile, the rows its walks visit most, else the
+//   shallowest states), the rest are renumbered by how many records fall
+//   back to them, so the fallback rows records use most have the smallest
+//   ids.
 //   Records: in the trie's order, at 8-B granules (state id = F + granule):
 //     word0 = out16 | c0 << 16 | c1 << 24   out16 = the record's OWN output
 //             (gid < 65536); c1 == c0 for one slot (a slotless record that
@@ -213,7 +214,19 @@ struct FlImage {
     uint32_t F = 0, granules = 0, folded = 0;
     uint32_t deep_g = 0;             // first granule of the deep records
 };
-bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl);
+// The profile text of the LDS-row choice: PM_FL_PROFILE_PIECES pieces of
+// PM_FL_PROFILE_PIECE bytes, walked from the root each; 15 of 16 are the
+// dictionary's own lines text (pm_streamgen.h pm_lines_block, seed 7: its
+// patterns drawn at random, '\n' after each), 1 of 16 random printable
+// ASCII (pm_stream_byte mode 0).  A function of the pattern list alone.
+constexpr size_t PM_FL_PROFILE_PIECES = 64, PM_FL_PROFILE_PIECE = 32 << 10;
+std::vector<uint8_t> pm_fl_profile(const std::vector<std::string>& pats);
+// With a profile, the LDS rows (the first PM_FL_LDS_ROWS) are the root and
+// the rows the profile's walks step from most -- row states and record
+// fallbacks -- instead of the root and the shallowest (scripts/
+// fl_rowline_model.cpp, snort: lines 0.209 -> 0.188 row and fallback
+// requests per step, random ASCII 0.477 -> 0.319).
+bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl, const std::vector<uint8_t>* profile = nullptr);
 // One FL step from state s with the word w that led to it (w = 0 at the
 // root) on byte c: returns the next word.  *out_prev = the output of the
 // position whose step produced w (s's own output when s is a record; w's

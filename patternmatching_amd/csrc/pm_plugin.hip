@@ -923,7 +923,8 @@ void pm_hip_compile(void* obj) {
                 }
             }
             FlImage fl;  // the fallback-linked form (pm_pack_sparse_fl)
-            if (pm_pack_sparse_fl(im.dfa, fl)) {
+            const std::vector<uint8_t> prof = pm_fl_profile(o->pats);  // the LDS rows' profile
+            if (pm_pack_sparse_fl(im.dfa, fl, &prof)) {
                 fl.block.resize(fl.block.size() + 16, 0u);  // the last aligned 32-B block
                 o->dfa.flbase = (const uint8_t*)dalloc_copy(o, fl.block.data(), fl.block.size() * 4);
                 o->dfa.flrowout16 = (const uint16_t*)dalloc_copy(o, fl.rowout16.data(), fl.rowout16.size() * 2);
@@ -1387,7 +1388,8 @@ void* pm_flat_build_cached(const char* const* pats, const uint32_t* lens, size_t
     h->dfa = std::move(im.dfa);
     h->par = std::move(im.par);
     if (!pm_pack_sparse8(h->dfa, h->block8, h->out8)) h->block8.clear(), h->out8.clear();
-    h->has_fl = pm_pack_sparse_fl(h->dfa, h->fl);
+    const std::vector<uint8_t> prof = pm_fl_profile(v);  // as compile() does
+    h->has_fl = pm_pack_sparse_fl(h->dfa, h->fl, &prof);
     return h;
 }
 

@@ -88,6 +88,11 @@ int main(int argc, char** argv) {
     const uint64_t SPREAD = (1ull << 30) / LANES;
     const int WARM = 256;
     std::vector<std::vector<uint8_t>> txt(LANES);
+    std::vector<uint8_t> ship;
+    if (getenv("SHIP")) {  // the reference's shipped stream, tiled
+        std::ifstream f(getenv("SHIP"), std::ios::binary);
+        ship.assign(std::istreambuf_iterator<char>(f), {});
+    }
     {
         std::vector<uint8_t> blk(PM_LINES_BLOCK);
         for (int L = 0; L < LANES; ++L) {
@@ -95,7 +100,8 @@ int main(int argc, char** argv) {
             for (uint64_t p = lo; p < lo + WARM + SEG; ++p) {
                 if (p % PM_LINES_BLOCK == 0 || p == lo)
                     pm_lines_block(blk.data(), PM_LINES_BLOCK, p / PM_LINES_BLOCK, P.data(), O.data(), pats.size(), 1);
-                txt[L].push_back(envi("ASCII", 0) ? pm_stream_byte(p, 1, 0) : blk[p % PM_LINES_BLOCK]);
+                txt[L].push_back(!ship.empty() ? ship[p % ship.size()]
+                                 : envi("ASCII", 0) ? pm_stream_byte(p, 1, 0) : blk[p % PM_LINES_BLOCK]);
             }
         }
     }
@@ -122,7 +128,68 @@ int main(int argc, char** argv) {
         roff[fl.granules] = off;
         printf("compact chains: records %.2f MB -> %.2f MB\n", fl.granules * 8 / 1e6, off / 1e6);
     }
-    for (int layout = 0; layout < 5; ++layout) {
+    // LDS row sets: the product's first KR rows, or (layouts 5, 6) the root
+    // and the KR-1 rows visited most on a separate sample of the same text
+    // (every row step and record-miss fallback counted)
+    std::vector<uint8_t> inlds(F, 0);
+    for (uint32_t r = 0; r < F && (int)r < KR; ++r) inlds[r] = 1;
+    std::vector<uint8_t> inlds_v(F, 0);
+    {
+        std::vector<uint64_t> vis(F, 0);
+        std::vector<uint32_t> w;
+        // the profile sample (MIX=1, the product's choice): 256 lanes of
+        // the dictionary's lines text and 256 of random printable ASCII,
+        // 4 KiB each, from offsets the evaluation does not use; else a
+        // quarter of the evaluation lanes themselves
+        const int MIX = envi("MIX", 1);
+        std::vector<std::vector<uint8_t>> smp;
+        if (MIX) {
+            std::vector<uint8_t> blk(PM_LINES_BLOCK);
+            for (int L = 0; L < 512; ++L) {
+                std::vector<uint8_t> t;
+                const uint64_t lo = (1ull << 40) + (uint64_t)L * (1 << 20);
+                for (uint64_t p = lo; p < lo + WARM + SEG; ++p) {
+                    if (L < (MIX == 2 ? 512 : envi("MIXL", 256))) {
+                        if (p % PM_LINES_BLOCK == 0 || p == lo)
+                            pm_lines_block(blk.data(), PM_LINES_BLOCK, p / PM_LINES_BLOCK, P.data(), O.data(), pats.size(), 7);
+                        t.push_back(blk[p % PM_LINES_BLOCK]);
+                    } else {
+                        t.push_back(pm_stream_byte(p, 7, 0));
+                    }
+                }
+                smp.push_back(t);
+            }
+        } else {
+            for (int L = 0; L < LANES; L += 4) smp.push_back(txt[L]);
+        }
+        w.assign(smp.size(), 0);
+        for (int j = 0; j < WARM + SEG; ++j)
+            for (size_t L = 0; L < smp.size(); ++L) {
+                const uint32_t c = smp[L][j];
+                const uint32_t s = w[L] & PM_DFA_STATE_MASK;
+                if (s < F) { vis[s]++; w[L] = B[(size_t)s * 256 + c]; continue; }
+                const uint32_t* U = B + (size_t)F * 256 + 2 * (size_t)(s - F);
+                if (c == ((U[0] >> 16) & 0xFFu)) w[L] = U[1];
+                else if (c == (U[0] >> 24)) w[L] = U[2];
+                else {
+                    const uint32_t fb = w[L] >> 20;
+                    const uint32_t row = fb == PM_FL_FB_INREC ? U[3] : fb;
+                    vis[row]++;
+                    w[L] = B[(size_t)row * 256 + c];
+                }
+            }
+        std::vector<uint32_t> ordr(F);
+        for (uint32_t r = 0; r < F; ++r) ordr[r] = r;
+        std::sort(ordr.begin(), ordr.end(), [&](uint32_t a, uint32_t b) { return vis[a] > vis[b]; });
+        inlds_v[0] = 1;
+        int k = 1;
+        for (uint32_t r : ordr) {
+            if (k >= KR) break;
+            if (!inlds_v[r]) { inlds_v[r] = 1; ++k; }
+        }
+    }
+    for (int layout = 0; layout < 6; ++layout) {
+        const std::vector<uint8_t>& lds = layout == 5 ? inlds_v : inlds;
         Lru l2{(size_t)L2KB * 1024 / 128};
         uint64_t rowreq = 0, recreq = 0, fbreq = 0, steps = 0, rowmiss = 0, recmiss = 0, fbmiss = 0;
         std::unordered_map<uint64_t, uint64_t> lines;
@@ -136,7 +203,7 @@ int main(int argc, char** argv) {
                 const uint32_t s = w[L] & PM_DFA_STATE_MASK;
                 uint32_t nw;
                 if (s < F) {
-                    if ((int)s >= KR) {
+                    if (!lds[s]) {
                         const uint64_t a = rowline(s, c);
                         const bool h = l2.touch(a);
                         if (cnt) { ++rowreq; rowmiss += !h; lines[a]++; }
@@ -160,7 +227,7 @@ int main(int argc, char** argv) {
                     else {
                         const uint32_t fb = w[L] >> 20;
                         const uint32_t row = fb == PM_FL_FB_INREC ? U[3] : fb;
-                        if ((int)row >= KR) {
+                        if (!lds[row]) {
                             const uint64_t a = rowline(row, c);
                             const bool h = l2.touch(a);
                             if (cnt) { ++fbreq; fbmiss += !h; lines[a]++; }
@@ -187,7 +254,7 @@ int main(int argc, char** argv) {
         }
         printf("%s: per step: row %.3f fallback %.3f record %.3f requests; L2 misses per step %.3f (row %.3f fb %.3f rec %.3f)\n"
                "   lines touched %zu (%.1f MB); 50/90/99%% of requests in %.2f / %.2f / %.2f MB\n",
-               layout == 4 ? "deep 128-B blocks" : layout == 3 ? "deep 64-B blocks" : layout == 2 ? "compact chains" : layout ? "permuted columns" : "product", (double)rowreq / steps, (double)fbreq / steps,
+               layout == 5 ? "LDS rows by visits" : layout == 4 ? "deep 128-B blocks" : layout == 3 ? "deep 64-B blocks" : layout == 2 ? "compact chains" : layout ? "permuted columns" : "product", (double)rowreq / steps, (double)fbreq / steps,
                (double)recreq / steps, (double)(rowmiss + fbmiss + recmiss) / steps, (double)rowmiss / steps,
                (double)fbmiss / steps, (double)recmiss / steps, h.size(), h.size() * 128 / 1e6, n50 * 128 / 1e6,
                n90 * 128 / 1e6, n99 * 128 / 1e6);
