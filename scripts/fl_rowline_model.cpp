@@ -8,6 +8,14 @@
 // step; the L2 is scaled with them (L2KB, default 512 = 4 MiB / 8).
 // Counts: row-word lines (rows past the KR in LDS), record lines (a new
 // 16-B half or 32-B block), fallback-row lines at a record miss.
+// Layouts (each line of output): the product image with its rows in BFS
+// order (pm_pack_sparse_fl without a profile); rows with their columns
+// permuted by byte frequency; unary-chain records in 4 B; deep records in
+// 64-B / 128-B blocks; the LDS rows chosen by visits on a profile sample
+// (MIX=1: MIXL of 512 lanes the dictionary's lines text, the rest random
+// ASCII -- the packer's profile is 15:1; MIX=2 lines only; MIX=0 the
+// evaluation text itself).  ASCII=1 / SHIP=<file>: evaluate on random
+// ASCII / a tiled file instead of the lines stream.
 //   g++ -O2 -std=c++17 -Ipatternmatching_amd/csrc -Iinclude scripts/fl_rowline_model.cpp \
 //       patternmatching_amd/csrc/pm_flatten.cpp patternmatching_amd/csrc/host/pm_dict.c -o /tmp/rowline && \
 //   /tmp/rowline tests/golden/data/snort.dict
