@@ -583,6 +583,7 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl, const std::vector<uint8_t
     std::vector<uint32_t> ord(F), nrow(F);
     for (uint32_t r = 0; r < F; ++r) ord[r] = r;
     const uint32_t keep = std::min(F, PM_FL_LDS_ROWS);
+    uint32_t kept = keep;  // rows whose order is fixed before the fallback-use sort
     if (profile && !profile->empty() && keep > 1) {
         // the rows the profile's walks step from (row states, and record
         // misses' fallback rows), one walk from the root per piece
@@ -607,9 +608,12 @@ bool pm_pack_sparse_fl(const DfaImage& d, FlImage& fl, const std::vector<uint8_t
         }
         vis[0] = ~0ull;  // the root stays row 0 (the warm-ups' start)
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return vis[a] > vis[b]; });
-        std::sort(ord.begin() + keep, ord.end());  // (the rest: by fallback use, next)
+        // the first PM_FL_COUNT_LDS_ROWS by visits (the count-only kernel
+        // stages that many; the others the first PM_FL_LDS_ROWS of them)
+        kept = std::min(F, PM_FL_COUNT_LDS_ROWS);
+        std::sort(ord.begin() + kept, ord.end());  // (the rest: by fallback use, next)
     }
-    std::stable_sort(ord.begin() + keep, ord.end(), [&](uint32_t a, uint32_t b) { return use[a] > use[b]; });
+    std::stable_sort(ord.begin() + kept, ord.end(), [&](uint32_t a, uint32_t b) { return use[a] > use[b]; });
     for (uint32_t k = 0; k < F; ++k) nrow[ord[k]] = k;
     // trie depth of every state, breadth first from the root: a row's
     // entries hold its goto children, a record's slots are all of its own

@@ -200,6 +200,7 @@ bool pm_pack_sparse8(const DfaImage& d, std::vector<uint32_t>& block8, std::vect
 // the 20-bit target field.
 constexpr uint32_t PM_FL_FB_INREC = 4095;  // the 12-bit field's top value
 constexpr uint32_t PM_FL_LDS_ROWS = 88;  // rows the kernel stages in LDS (dfa_fl_kernel<88>)
+constexpr uint32_t PM_FL_COUNT_LDS_ROWS = 156;  // ... its count-only instance (no staging rows)
 // Records of trie depth < PM_FL_DEEP_DEPTH come first (the kernel loads
 // them as 16-B halves: a walk rarely stays), then, from granule deep_g (a
 // multiple of 8), the deeper ones (loaded as aligned 32-B blocks: a walk

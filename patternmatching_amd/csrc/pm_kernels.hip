@@ -1199,7 +1199,8 @@ constexpr uint32_t DFA_ESC = 4095u;
 constexpr uint32_t PM_FL_INREC = 4095u;  // must match pm_flatten.h PM_FL_FB_INREC
 constexpr int FL_LDS_ROWS = 88;          // must match pm_flatten.h PM_FL_LDS_ROWS
 // The count-only FL kernel has no staging rows: 156 rows fill the LDS (the
-// 88 shallowest, then the fallbacks records use most: pm_pack_sparse_fl's order).
+// root and the rows pm_pack_sparse_fl's profile visits most; must match
+// pm_flatten.h PM_FL_COUNT_LDS_ROWS).
 constexpr int FL_COUNT_LDS_ROWS = 156;
 
 // The start of the last synchronizing 3-gram in [wlo, lo - 3], or wlo when
