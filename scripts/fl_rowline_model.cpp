@@ -15,7 +15,9 @@
 // (MIX=1: MIXL of 512 lanes the dictionary's lines text, the rest random
 // ASCII -- the packer's profile is 15:1; MIX=2 lines only; MIX=0 the
 // evaluation text itself).  ASCII=1 / SHIP=<file>: evaluate on random
-// ASCII / a tiled file instead of the lines stream.
+// ASCII / a tiled file instead of the lines stream.  COVER=1: instead, the
+// share of non-root row requests LDS would serve holding whole rows, hot
+// 128-B row lines, or rows' printable lines, chosen on the profile.
 //   g++ -O2 -std=c++17 -Ipatternmatching_amd/csrc -Iinclude scripts/fl_rowline_model.cpp \
 //       patternmatching_amd/csrc/pm_flatten.cpp patternmatching_amd/csrc/host/pm_dict.c -o /tmp/rowline && \
 //   /tmp/rowline tests/golden/data/snort.dict
@@ -195,6 +197,82 @@ int main(int argc, char** argv) {
             if (k >= KR) break;
             if (!inlds_v[r]) { inlds_v[r] = 1; ++k; }
         }
+    }
+    if (envi("COVER", 0)) {
+        // row and fallback-row requests by (row, 128-B line), profile vs evaluation
+        auto walk = [&](const std::vector<std::vector<uint8_t>>& T, std::unordered_map<uint64_t, uint64_t>& cnt) {
+            std::vector<uint32_t> w(T.size(), 0);
+            for (int j = 0; j < WARM + SEG; ++j)
+                for (size_t L = 0; L < T.size(); ++L) {
+                    const uint32_t c = T[L][j];
+                    const uint32_t s = w[L] & PM_DFA_STATE_MASK;
+                    uint32_t row = s;
+                    if (s >= F) {
+                        const uint32_t* U = B + (size_t)F * 256 + 2 * (size_t)(s - F);
+                        if (c == ((U[0] >> 16) & 0xFFu)) { w[L] = U[1]; continue; }
+                        if (c == (U[0] >> 24)) { w[L] = U[2]; continue; }
+                        const uint32_t fb = w[L] >> 20;
+                        row = fb == PM_FL_FB_INREC ? U[3] : fb;
+                    }
+                    if (row != 0 && j >= WARM) cnt[(uint64_t)row * 8 + (c >> 5)]++;
+                    w[L] = B[(size_t)row * 256 + c];
+                }
+        };
+        std::vector<std::vector<uint8_t>> prof;
+        {
+            std::vector<uint8_t> blk(PM_LINES_BLOCK);
+            for (int L = 0; L < 512; ++L) {
+                std::vector<uint8_t> t;
+                const uint64_t lo = (1ull << 40) + (uint64_t)L * (1 << 20);
+                for (uint64_t p = lo; p < lo + WARM + SEG; ++p) {
+                    if (L < 480) {
+                        if (p % PM_LINES_BLOCK == 0 || p == lo)
+                            pm_lines_block(blk.data(), PM_LINES_BLOCK, p / PM_LINES_BLOCK, P.data(), O.data(), pats.size(), 7);
+                        t.push_back(blk[p % PM_LINES_BLOCK]);
+                    } else t.push_back(pm_stream_byte(p, 7, 0));
+                }
+                prof.push_back(t);
+            }
+        }
+        std::unordered_map<uint64_t, uint64_t> pc, ec;
+        walk(prof, pc);
+        walk(txt, ec);
+        uint64_t tot = 0;
+        for (auto& x : ec) tot += x.second;
+        // whole rows: top K by profile visits (sum over lines), lines: top N pairs
+        std::unordered_map<uint32_t, uint64_t> rv;
+        for (auto& x : pc) rv[(uint32_t)(x.first / 8)] += x.second;
+        std::vector<std::pair<uint64_t, uint32_t>> rows;
+        for (auto& x : rv) rows.push_back({x.second, x.first});
+        std::sort(rows.rbegin(), rows.rend());
+        std::vector<std::pair<uint64_t, uint64_t>> lns;
+        for (auto& x : pc) lns.push_back({x.second, x.first});
+        std::sort(lns.rbegin(), lns.rend());
+        for (int K : {87, 150}) {
+            std::unordered_map<uint32_t, int> in;
+            for (int k = 0; k < K && k < (int)rows.size(); ++k) in[rows[k].second] = 1;
+            uint64_t cov = 0;
+            for (auto& x : ec) if (in.count((uint32_t)(x.first / 8))) cov += x.second;
+            printf("whole rows %d (%d KiB): %.1f%% of non-root row requests\n", K, K, 100.0 * cov / tot);
+        }
+        for (int K : {234, 300}) {  // rows' printable lines only (bytes 32-127: 3 lines, 384 B a row)
+            std::unordered_map<uint32_t, int> in;
+            for (int k = 0; k < K && k < (int)rows.size(); ++k) in[rows[k].second] = 1;
+            uint64_t cov = 0;
+            for (auto& x : ec) {
+                const uint32_t ln = (uint32_t)(x.first % 8);
+                if (in.count((uint32_t)(x.first / 8)) && ln >= 1 && ln <= 3) cov += x.second;
+            }
+            printf("printable lines of %d rows (%d KiB): %.1f%% of non-root row requests\n", K, K * 3 / 8, 100.0 * cov / tot);
+        }
+        for (int N : {340, 680, 1200}) {
+            std::unordered_map<uint64_t, int> in;
+            for (int k = 0; k < N && k < (int)lns.size(); ++k) in[lns[k].second] = 1;
+            uint64_t cov = 0;
+            for (auto& x : ec) if (in.count(x.first)) cov += x.second;
+            printf("row lines %d (%d KiB): %.1f%% of non-root row requests\n", N, N / 8, 100.0 * cov / tot);
+        }
+        return 0;
     }
     for (int layout = 0; layout < 6; ++layout) {
         const std::vector<uint8_t>& lds = layout == 5 ? inlds_v : inlds;
