@@ -143,6 +143,11 @@ for ev, tag in ((0, ""), (1, "_events")):
         res[f"read_block_ids{kname}{tag}_us"] = timeit(call_ids(mm))
         mm.set_option("host_events", -1)
     res[f"read_block_gid{tag}_GBps"] = round(N / res[f"read_block_gid{tag}_us"] / 1e3, 3)
+for g16 in (1, 0):  # u16 gids over the link, widened on the host pool
+    assert m.set_option("host_gid16", g16) == 0
+    m.reset()
+    res[f"read_block_gid_gid16_{g16}_us"] = timeit(call)
+m.set_option("host_gid16", -1)
 dst = np.empty(N, np.int32)
 hn = hout.numpy()
 res["host_copy_400k_us"] = timeit(lambda: np.copyto(dst, hn))
