@@ -73,6 +73,12 @@ enum Kind { KIND_RT = 1, KIND_AC = 2, KIND_AUTO = 3 };
 constexpr double AUTO_SPILL_FRAC = 0.10;
 constexpr int AUTO_TRIAL = 2;
 constexpr int AUTO_HOLD = 64;
+// A choice that the next measurement confirms is held twice as long (up to
+// AUTO_HOLD << AUTO_STREAK_MAX launches): on a long deep stream each
+// measurement costs an RT launch and the DFA trials -- on the lines stream
+// ~3x and ~1-3.5x the held kernel's time -- so a fixed hold of 64 launches
+// spent ~20% of the time measuring.  reset() (a new stream) starts over.
+constexpr int AUTO_STREAK_MAX = 6;
 // CAND_SPARSE16: the sparse form's fallback-linked kernel holding every
 // record as a 16-B half (FlImage::deep_g ignored): faster where walks
 // rarely stay in a record's block (the tiled shipped stream: 3.53 -> 3.36
@@ -94,6 +100,8 @@ struct AutoPick {
     double ns[NCAND] = {};    // measured ns per position (0 = not measured this round)
     int hold = 0;             // launches left on the chosen candidate
     int chosen = CAND_RT;
+    int prev = -1;            // the choice the previous measurement made
+    int streak = 0;           // measurements in a row that made the same choice
     int last = 0;             // KIND_RT / KIND_AC of the last launch
     int last_form = 0;        // DFA form of the last launch: 1 dense rows, 2 sparse (0: RT)
 };
@@ -226,6 +234,8 @@ void forget_pick(AutoPick& a) {
     a.pending = a.timing = false;
     a.nq = a.qi = a.trial = 0;
     a.hold = 0;
+    a.prev = -1;
+    a.streak = 0;
 }
 
 void free_pick(AutoPick& a) {
@@ -560,6 +570,13 @@ void start_trials(const PmHip* o, AutoPick& ap) {
     ap.trial = 0;
 }
 
+// The hold after a measurement chose ap.chosen (AUTO_STREAK_MAX).
+int confirm_hold(AutoPick& ap) {
+    ap.streak = ap.chosen == ap.prev ? std::min(ap.streak + 1, AUTO_STREAK_MAX) : 0;
+    ap.prev = ap.chosen;
+    return AUTO_HOLD << ap.streak;
+}
+
 // Fold in whatever measurement has landed (KIND_AUTO / KIND_AC, see
 // AUTO_SPILL_FRAC).
 void resolve_pick(const PmHip* o, AutoPick& ap) {
@@ -577,7 +594,7 @@ void resolve_pick(const PmHip* o, AutoPick& ap) {
             start_trials(o, ap);
         } else {  // shallow: RT holds
             ap.chosen = CAND_RT;
-            ap.hold = AUTO_HOLD;
+            ap.hold = confirm_hold(ap);
         }
     }
     auto trials_done = [&]() {  // every trial's end event (they may sit on different streams)
@@ -598,7 +615,7 @@ void resolve_pick(const PmHip* o, AutoPick& ap) {
             }
         }
         ap.chosen = best;
-        ap.hold = AUTO_HOLD;
+        ap.hold = confirm_hold(ap);
         ap.nq = ap.qi = 0;
     }
 }

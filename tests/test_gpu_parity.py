@@ -1456,6 +1456,34 @@ def test_auto_count_only_follows_deep_walks():
             assert kernels == [pm.KIND_RT] * 3, kernels
 
 
+def test_auto_hold_doubles_when_confirmed():
+    """The auto kind re-measures (an RT launch, then the DFA trials) after
+    its hold; a choice the next measurement confirms is held twice as long
+    (pm_plugin.hip AUTO_STREAK_MAX), so on a deep stream the RT launches
+    come further apart; every launch stays exact."""
+    import torch
+    n = 16 << 20  # the tiled shipped stream: a DFA form holds, so each RT launch is a measurement
+    s = torch.cuda.current_stream()
+    rt, au = matcher("et", "rt"), matcher("et", "auto")
+    dt = torch.from_numpy(np.concatenate([_tiled_ship(n), np.zeros(64, np.uint8)])).cuda()
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    rt.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
+    au.reset()
+    kinds = []
+    got = torch.empty(n, dtype=torch.int32, device="cuda")
+    for k in range(260):
+        au.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
+        torch.cuda.synchronize()
+        kinds.append(au.kernel_last)
+        if k % 37 == 0:
+            assert torch.equal(got, want), k
+    rts = [k for k, v in enumerate(kinds) if v == pm.KIND_RT]
+    assert rts[0] == 0 and len(rts) >= 3 and kinds[10] == pm.KIND_AC, (rts, kinds[:12])
+    gaps = [b - a for a, b in zip(rts, rts[1:])]
+    assert gaps[1] > gaps[0] + 32, (rts, gaps)
+    au.reset()
+
+
 def test_auto_stays_on_rt_for_sparse_matches():
     import torch
     n = 16 << 20
