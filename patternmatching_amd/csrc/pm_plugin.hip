@@ -560,12 +560,15 @@ hipError_t launch_cand(PmHip* o, AutoPick& ap, int c, const uint8_t* text, int64
 // The DFA forms to try, in order (dense rows, then rows + records; only the
 // object's forced form when it has one).
 void start_trials(const PmHip* o, AutoPick& ap) {
+    // (the last one queued also runs while the trials' times are in flight:
+    // a caller far ahead of the device launches it until they land, so the
+    // usual winner on deep input goes last)
     ap.nq = 0;
     if (o->dfa_form != 2 || !o->dfa.sbase) ap.queue[ap.nq++] = CAND_DENSE;
-    if (o->dfa.sbase && o->dfa_form != 1) ap.queue[ap.nq++] = CAND_SPARSE;
     if (o->dfa.flbase && o->dfa_form != 1 &&
         (o->dfa.sparse_kernel == PM_SK_PRODUCT || o->dfa.sparse_kernel == PM_SK_FL))
         ap.queue[ap.nq++] = CAND_SPARSE16;
+    if (o->dfa.sbase && o->dfa_form != 1) ap.queue[ap.nq++] = CAND_SPARSE;
     ap.qi = 0;
     ap.trial = 0;
 }
