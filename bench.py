@@ -46,7 +46,8 @@ DATA = os.path.join(REPO, "tests", "golden", "data")
 DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "et.dict"]}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 WIDTH = {"dense": 4, "dense16": 2, "count": 0}  # bytes written per stream position
-CAND_NAME = {0: "RT", 1: "RT", 2: "AC dense rows", 3: "AC rows + records", 4: "AC rows + records (16-B record loads)"}
+CAND_NAME = {0: "RT", 1: "RT", 2: "AC dense rows", 3: "AC rows + records", 4: "AC rows + records (16-B record loads)",
+             5: "AC rows + records (64-B deep blocks)"}
 # a reference AC object per CPU-baseline process: snort's table is ~1.06 GB
 # (2072 B per state, mpac.c:43-48), so the process count is also bounded by memory
 REF_PROC_BYTES = 1_300_000_000

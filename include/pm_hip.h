@@ -113,7 +113,8 @@ int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, un
  * (pm_hip_auto_create) for at least the next `launches` launches, so a timed
  * region never re-measures.  Returns the held kernel (1 = reverse trie,
  * 2 = AC dense rows, 3 = AC rows + records, 4 = the same with every record
- * loaded as a 16-B half), 0 when the object has no choice
+ * loaded as a 16-B half, 5 = the same with deep records' 64-B blocks), 0
+ * when the object has no choice
  * to make (rt kind, or a single DFA form), -1 while the pick is still being
  * measured (launch more, synchronize, and ask again). */
 int pm_hip_hold_choice(void* obj, int launches);
@@ -205,6 +206,10 @@ int pm_hip_set_device(int device);
  *                     8-B units, 4 = lock-step 8-B units, 5 = lock-step 16-B
  *                     records; a launch the object or width cannot run with
  *                     the forced kernel fails (-3)
+ *   "fl_hold"         the fallback-linked kernel's record loads outside the
+ *                     picks' trials: 2 = deep records' 32-B blocks (0, the
+ *                     default), 4 = 64-B blocks, 1 = every record as a 16-B
+ *                     half (the ac / auto picks time all three)
  *   "dfa_sync"        1 = DFA warm-ups start at the last synchronizing 3-gram
  *                     (default), 0 = max_len - 1 bytes back
  *   "rt_small_max"    reverse-trie launches of at most this many positions

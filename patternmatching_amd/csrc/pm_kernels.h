@@ -75,6 +75,10 @@ struct DfaDev {
     uint32_t flF;
     uint32_t flGD;  // first deep granule (pm_flatten.h FlImage::deep_g)
     uint32_t flwords;  // 4-B words of the FL image (rows, then records)
+    // 16-B registers a lane holds of a deep record's block: 2 (32-B blocks,
+    // the default), 4 (64-B blocks) or 1 (every record as a 16-B half,
+    // flGD ignored); the auto / ac picks time all three
+    int flhold = 2;
 };
 
 // Positions [pos0, pos0+n) of text; bytes back to stream_start are context.

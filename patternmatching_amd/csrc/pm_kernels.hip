@@ -1880,33 +1880,36 @@ __device__ __forceinline__ int64_t wave_uniform64(int64_t v) {
 static_assert(PM_FL_SPEC == 0 || PM_FL_SPEC == 2, "PM_FL_SPEC: 0 (product) or 2 (ablation)");
 
 // A lane holds the records around its state: for a shallow record (granule
-// below GD, pm_flatten.h FlImage::deep_g) the 16-B half holding it, in R0;
-// for a deep one the aligned 32-B block, R0 and R1.  The held key: the
-// half's index, or the block's with the top bit set.
-// The deep records' block: PM_FL_DEEP_BLK bytes (32, the product, or 64 --
-// an ablation build), NR 16-B registers.
-#ifndef PM_FL_DEEP_BLK
-#define PM_FL_DEEP_BLK 32
-#endif
-static_assert(PM_FL_DEEP_BLK == 32 || PM_FL_DEEP_BLK == 64, "PM_FL_DEEP_BLK: 32 or 64");
-constexpr int FL_NR = PM_FL_DEEP_BLK / 16;
-constexpr uint32_t FL_DSHIFT = PM_FL_DEEP_BLK == 64 ? 3u : 2u;  // granules per deep block: 4 or 8
+// below GD, pm_flatten.h FlImage::deep_g) the 16-B half holding it, in
+// R[0]; for a deep one the aligned block of NR 16-B halves (NR 2: 32 B, the
+// default; 4: 64 B; 1: every record as a half, GD ignored -- DfaDev::flhold,
+// the picks time all three).  The held key: the half's index, or the
+// block's with the top bit set.
+template <int NR>
 struct FlHold {
-    tu32x4 R[FL_NR];
+    tu32x4 R[NR];
 };
 
-__device__ __forceinline__ uint32_t fl_key(uint32_t g, bool deep) {
-    return deep ? (g >> FL_DSHIFT) | 0x80000000u : g >> 1;
+template <int NR>
+__device__ __forceinline__ bool fl_deep(uint32_t g, uint32_t GD) {
+    return NR > 1 && g >= GD;
 }
 
+template <int NR>
+__device__ __forceinline__ uint32_t fl_key(uint32_t g, bool deep) {
+    constexpr uint32_t DSHIFT = NR == 4 ? 3u : 2u;  // granules per deep block: 8 or 4
+    return deep ? (g >> DSHIFT) | 0x80000000u : g >> 1;
+}
+
+template <int NR>
 __device__ __forceinline__ void fl_load(const uint8_t* __restrict__ base, uint32_t F, uint32_t g, bool deep,
-                                        FlHold& H) {
+                                        FlHold<NR>& H) {
     const tu32x4* p =
-        reinterpret_cast<const tu32x4*>(base + F * 1024u + ((g >> 1) & (deep ? ~(uint32_t)(FL_NR - 1) : ~0u)) * 16u);
+        reinterpret_cast<const tu32x4*>(base + F * 1024u + ((g >> 1) & (deep ? ~(uint32_t)(NR - 1) : ~0u)) * 16u);
     H.R[0] = p[0];
     if (deep) {
 #pragma unroll
-        for (int k = 1; k < FL_NR; ++k) H.R[k] = p[k];
+        for (int k = 1; k < NR; ++k) H.R[k] = p[k];
     }
 }
 
@@ -1915,22 +1918,24 @@ __device__ __forceinline__ tu32x4 bsel4(uint32_t m, const tu32x4& a, const tu32x
 }
 
 // The 16-B register holding granule g (a shallow half is always R[0]).
-__device__ __forceinline__ tu32x4 fl_reg(const FlHold& H, uint32_t g, bool deep) {
+template <int NR>
+__device__ __forceinline__ tu32x4 fl_reg(const FlHold<NR>& H, uint32_t g, bool deep) {
+    if (NR == 1) return H.R[0];
     const uint32_t m2 = bmask(deep && (g & 2u));
-    if (FL_NR == 2) return bsel4(m2, H.R[0], H.R[FL_NR - 1]);
+    if (NR == 2) return bsel4(m2, H.R[0], H.R[NR - 1]);
     const uint32_t m4 = bmask(deep && (g & 4u));
-    return bsel4(m4, bsel4(m2, H.R[0], H.R[1 % FL_NR]), bsel4(m2, H.R[2 % FL_NR], H.R[3 % FL_NR]));
+    return bsel4(m4, bsel4(m2, H.R[0], H.R[1 % NR]), bsel4(m2, H.R[2 % NR], H.R[3 % NR]));
 }
 
-template <int KR>
+template <int KR, int NR>
 __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
                                             const uint32_t* __restrict__ s_rows, uint32_t w, uint32_t c,
-                                            uint32_t& cb, FlHold& H, uint32_t& own) {
+                                            uint32_t& cb, FlHold<NR>& H, uint32_t& own) {
     const uint32_t s = w & DFA_STATE_MASK;
     const bool isrow = s < F;
     const uint32_t g = s - F;
-    const bool deep = g >= GD;
-    const uint32_t key = fl_key(g, deep);
+    const bool deep = fl_deep<NR>(g, GD);
+    const uint32_t key = fl_key<NR>(g, deep);
     const uint32_t fb = w >> 20;
     const bool newblk = !isrow && key != cb;
     const bool pre = PM_FL_SPEC == 2 && newblk && fb != PM_FL_INREC && fb >= (uint32_t)KR;
@@ -1966,8 +1971,9 @@ __device__ __forceinline__ uint32_t fl_step(const uint8_t* __restrict__ base, ui
 // holds it loaded if the lane does not hold it -- the next step's load,
 // made early), or a row word's code; *esc = the code escapes (the answer
 // is then rowout16[w & MASK]).
+template <int NR>
 __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, uint32_t F, uint32_t GD, uint32_t w,
-                                              uint32_t& cb, FlHold& H, bool& esc) {
+                                              uint32_t& cb, FlHold<NR>& H, bool& esc) {
     const uint32_t s = w & DFA_STATE_MASK;
     esc = false;
     if (s < F) {
@@ -1975,8 +1981,8 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
         return w >> 20;
     }
     const uint32_t g = s - F;
-    const bool deep = g >= GD;
-    const uint32_t key = fl_key(g, deep);
+    const bool deep = fl_deep<NR>(g, GD);
+    const uint32_t key = fl_key<NR>(g, deep);
     if (key != cb) {
         fl_load(base, F, g, deep, H);
         cb = key;
@@ -1992,15 +1998,14 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
 // (the state it starts from holds it).  OUTW 4 / 2: u32 / u16 ids (a u16
 // block of a chain is 64 B: four lanes' 16-B stores, 16 chains per store
 // instruction); 0: the count alone, no staging rows, no escapes, no stores.
-// H16: every record held as a 16-B half (the picks' CAND_SPARSE16 trial;
-// its own instance, so profiles tell it from the product's launches).
-template <int KR, int OUTW = 4, bool H16 = false>
+// NR: the 16-B halves a lane holds of a deep block (FlHold; each its own
+// instance, so profiles tell the picks' trials from the default's launches).
+template <int KR, int OUTW = 4, int NR = 2>
 __global__ __launch_bounds__(1024) void dfa_fl_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
     const uint16_t* __restrict__ rowout16, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
     static_assert(OUTW == 0 || OUTW == 2 || OUTW == 4, "u32 / u16 ids or the count");
-    if (H16) GD = 0xFFFFFFFFu;
     constexpr int THREADS = 1024, BLK = 32, SROW = 17;
     constexpr bool kIds = OUTW != 0;
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
@@ -2018,9 +2023,9 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
     const int64_t nseg = (n + seg_len - 1) / seg_len;
     const int64_t lanes = (int64_t)gridDim.x * THREADS;
     uint32_t cnt = 0, cb = 0xFFFFFFFFu, own = 0;
-    FlHold H;
+    FlHold<NR> H;
 #pragma unroll
-    for (int k = 0; k < FL_NR; ++k) H.R[k] = tu32x4{0u, 0u, 0u, 0u};
+    for (int k = 0; k < NR; ++k) H.R[k] = tu32x4{0u, 0u, 0u, 0u};
     for (int64_t sg0 = (int64_t)blockIdx.x * THREADS + threadIdx.x; __ballot(sg0 < nseg); sg0 += lanes) {
         const bool has = sg0 < nseg;
         // the wave's segments are consecutive: a wave-uniform 64-bit base
@@ -2034,7 +2039,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
         int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
         if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
         uint32_t w = 0;  // the root, reached by no word
-        for (int64_t i = wlo; i < lo; ++i) w = fl_step<KR>(base, F, GD, s_rows, w, text[i], cb, H, own);
+        for (int64_t i = wlo; i < lo; ++i) w = fl_step<KR, NR>(base, F, GD, s_rows, w, text[i], cb, H, own);
         const int64_t nblk = seg_len / BLK;
         for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
             bool act[2];
@@ -2061,7 +2066,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 uint32_t em = 0;
 #pragma unroll
                 for (int j = 0; j < BLK; ++j) {
-                    const uint32_t wn = fl_step<KR>(base, F, GD, s_rows, w, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb,
+                    const uint32_t wn = fl_step<KR, NR>(base, F, GD, s_rows, w, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb,
                                                     H, own);
                     if (j > 0) {  // the output of position j - 1, which produced w
                         const bool rec = (w & DFA_STATE_MASK) >= F;
@@ -2110,32 +2115,39 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 const uint64_t mine = am >> (lane / LPC);  // bit CPI * t: chain of store t active
                 const bool full = am == ~0ull;
                 const uint8_t* const lb = reinterpret_cast<const uint8_t*>(wrows) + lds_off;
-                tu32x4 vs[NST];  // every store's ids read first (one LDS wait), inactive chains too
+                // every store's ids read first (one LDS wait per batch),
+                // inactive chains too; two batches where the lane holds 64-B
+                // blocks (registers)
+                constexpr int NBAT = NR == 4 ? 2 : 1, BST = NST / NBAT;
 #pragma unroll
-                for (int t = 0; t < NST; ++t) {
-                    const uint32_t* src = reinterpret_cast<const uint32_t*>(lb + t * CPI * SROW * 4);
-                    if (OUTW == 4) {
-                        const uint32_t w0 = src[0], w1 = src[1];
-                        vs[t] = tu32x4{w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
-                    } else {
-                        vs[t] = tu32x4{src[0], src[1], src[2], src[3]};
+                for (int t0 = 0; t0 < NST; t0 += BST) {
+                    tu32x4 vs[BST];
+#pragma unroll
+                    for (int t = t0; t < t0 + BST; ++t) {
+                        const uint32_t* src = reinterpret_cast<const uint32_t*>(lb + t * CPI * SROW * 4);
+                        if (OUTW == 4) {
+                            const uint32_t w0 = src[0], w1 = src[1];
+                            vs[t - t0] = tu32x4{w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
+                        } else {
+                            vs[t - t0] = tu32x4{src[0], src[1], src[2], src[3]};
+                        }
                     }
-                }
 #pragma unroll
-                for (int t = 0; t < NST; ++t) {
-                    const tu32x4 v = vs[t];
-                    const int64_t step = (int64_t)(CPI * t) * seg_len + BLK * b;  // wave-uniform
-                    tu32x4* o = OUTW == 4
-                                    ? reinterpret_cast<tu32x4*>(reinterpret_cast<uint32_t*>(out) + wseg * seg_len + step + go)
-                                    : reinterpret_cast<tu32x4*>(reinterpret_cast<uint16_t*>(out) + wseg * seg_len + step + go);
-                    if (full || ((mine >> (CPI * t)) & 1u)) __builtin_nontemporal_store(v, o);
+                    for (int t = t0; t < t0 + BST; ++t) {
+                        const tu32x4 v = vs[t - t0];
+                        const int64_t step = (int64_t)(CPI * t) * seg_len + BLK * b;  // wave-uniform
+                        tu32x4* o = OUTW == 4
+                                        ? reinterpret_cast<tu32x4*>(reinterpret_cast<uint32_t*>(out) + wseg * seg_len + step + go)
+                                        : reinterpret_cast<tu32x4*>(reinterpret_cast<uint16_t*>(out) + wseg * seg_len + step + go);
+                        if (full || ((mine >> (CPI * t)) & 1u)) __builtin_nontemporal_store(v, o);
+                    }
                 }
                 __builtin_amdgcn_wave_barrier();
             });
         }
         // the segment's last (< BLK) positions
         for (int64_t i = lo + BLK * ((hi - lo) / BLK); i < hi; ++i) {
-            w = fl_step<KR>(base, F, GD, s_rows, w, text[i], cb, H, own);
+            w = fl_step<KR, NR>(base, F, GD, s_rows, w, text[i], cb, H, own);
             bool esc;
             uint32_t id = fl_output(base, F, GD, w, cb, H, esc);
             if (kIds && esc) id = rowout16[w & DFA_STATE_MASK];
@@ -2499,18 +2511,19 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         const dim3 gs((unsigned)wg), bs(wgt);
         switch (sk) {
             case PM_SK_FL:
-#define PM_FL_LAUNCH(KR_, W_, H_)                                                                                  \
-    hipLaunchKernelGGL((dfa_fl_kernel<KR_, W_, H_>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, t.flbase, \
+#define PM_FL_LAUNCH(KR_, W_, NR_)                                                                                  \
+    hipLaunchKernelGGL((dfa_fl_kernel<KR_, W_, NR_>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, t.flbase, \
                        t.flF, t.flGD, t.flrowout16, t.warm, seg, g3)
-                if (t.flGD == 0xFFFFFFFFu) {  // every record as a 16-B half
-                    if (outw == 4) PM_FL_LAUNCH(FL_LDS_ROWS, 4, true);
-                    else if (outw == 2) PM_FL_LAUNCH(FL_LDS_ROWS, 2, true);
-                    else PM_FL_LAUNCH(FL_COUNT_LDS_ROWS, 0, true);
-                } else {
-                    if (outw == 4) PM_FL_LAUNCH(FL_LDS_ROWS, 4, false);
-                    else if (outw == 2) PM_FL_LAUNCH(FL_LDS_ROWS, 2, false);
-                    else PM_FL_LAUNCH(FL_COUNT_LDS_ROWS, 0, false);
-                }
+#define PM_FL_WIDTHS(NR_)                                       \
+    do {                                                        \
+        if (outw == 4) PM_FL_LAUNCH(FL_LDS_ROWS, 4, NR_);       \
+        else if (outw == 2) PM_FL_LAUNCH(FL_LDS_ROWS, 2, NR_);  \
+        else PM_FL_LAUNCH(FL_COUNT_LDS_ROWS, 0, NR_);           \
+    } while (0)
+                if (t.flhold == 1) PM_FL_WIDTHS(1);  // every record as a 16-B half
+                else if (t.flhold == 4) PM_FL_WIDTHS(4);  // 64-B deep blocks
+                else PM_FL_WIDTHS(2);
+#undef PM_FL_WIDTHS
 #undef PM_FL_LAUNCH
                 break;
             case PM_SK_STAGE16:

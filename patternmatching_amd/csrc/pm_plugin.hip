@@ -80,11 +80,15 @@ constexpr int AUTO_HOLD = 64;
 // spent ~20% of the time measuring.  reset() (a new stream) starts over.
 constexpr int AUTO_STREAK_MAX = 6;
 // CAND_SPARSE16: the sparse form's fallback-linked kernel holding every
-// record as a 16-B half (FlImage::deep_g ignored): faster where walks
-// rarely stay in a record's block (the tiled shipped stream: 3.53 -> 3.36
-// ms, snort, profiles/r05/ab/fl_depth_split.jsonl), slower on the lines
-// stream (5.07 -> 5.54); timed beside the other forms.
-enum Cand { CAND_RT = 0, CAND_DENSE = 1, CAND_SPARSE = 2, CAND_SPARSE16 = 3, NCAND = 4 };
+// record as a 16-B half (DfaDev::flhold 1, FlImage::deep_g ignored): faster
+// where walks rarely stay in a record's block (snort, the tiled shipped
+// stream 3.48 -> 3.24 ms, ASCII 2.90 -> 2.78), slower on the lines stream
+// (4.99 -> 5.42).  CAND_SPARSE64: the same kernel holding deep records'
+// 64-B blocks (flhold 4): faster where walks run down long chains (snort
+// lines 4.99 -> 4.87, merged lines 5.43 -> 5.13), slower elsewhere (shipped
+// 3.64, ASCII 3.07).  profiles/r05/ab/fl_hold_1_2_4.jsonl; all three timed
+// beside the other forms.
+enum Cand { CAND_RT = 0, CAND_DENSE = 1, CAND_SPARSE = 2, CAND_SPARSE16 = 3, CAND_SPARSE64 = 4, NCAND = 5 };
 
 struct AutoPick {
     unsigned long long* d_spill = nullptr;  // device counter of the last measured RT launch
@@ -93,7 +97,7 @@ struct AutoPick {
     hipEvent_t t0[NCAND] = {}, t1[NCAND] = {};  // timing of each candidate's measured launch
     bool pending = false;     // a measured RT launch (spill count + time) in flight
     bool timing = false;      // the DFA trials are launched, their times in flight
-    int queue[3] = {0, 0, 0};  // DFA forms to try, in order
+    int queue[4] = {0, 0, 0, 0};  // DFA forms to try, in order
     int nq = 0, qi = 0;       // forms queued / started
     int trial = 0;            // launches left of the form being tried (the last one timed)
     int64_t n_of[NCAND] = {};
@@ -552,7 +556,8 @@ hipError_t launch_cand(PmHip* o, AutoPick& ap, int c, const uint8_t* text, int64
     if (c == CAND_RT) return pm_launch_rt(text, stream_start, pos0, n, out, outw, count, t, o->num_cu, s);
     DfaDev d = o->dfa;
     d.form = c == CAND_DENSE ? 1 : 2;
-    if (c == CAND_SPARSE16) d.flGD = 0xFFFFFFFFu;
+    if (c == CAND_SPARSE16) d.flhold = 1;
+    if (c == CAND_SPARSE64) d.flhold = 4;
     o->last_sparse_kernel = pm_dfa_sparse_choice(d, out ? outw : 0);
     return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, d, o->num_cu, s);
 }
@@ -564,11 +569,12 @@ void start_trials(const PmHip* o, AutoPick& ap) {
     // a caller far ahead of the device launches it until they land, so the
     // usual winner on deep input goes last)
     ap.nq = 0;
+    const bool fl = o->dfa.flbase && o->dfa_form != 1 &&
+                    (o->dfa.sparse_kernel == PM_SK_PRODUCT || o->dfa.sparse_kernel == PM_SK_FL);
     if (o->dfa_form != 2 || !o->dfa.sbase) ap.queue[ap.nq++] = CAND_DENSE;
-    if (o->dfa.flbase && o->dfa_form != 1 &&
-        (o->dfa.sparse_kernel == PM_SK_PRODUCT || o->dfa.sparse_kernel == PM_SK_FL))
-        ap.queue[ap.nq++] = CAND_SPARSE16;
+    if (fl) ap.queue[ap.nq++] = CAND_SPARSE16;
     if (o->dfa.sbase && o->dfa_form != 1) ap.queue[ap.nq++] = CAND_SPARSE;
+    if (fl) ap.queue[ap.nq++] = CAND_SPARSE64;
     ap.qi = 0;
     ap.trial = 0;
 }
@@ -1251,6 +1257,11 @@ int pm_hip_set_option(void* obj, const char* name, int64_t value) {
     if (k == "sparse_kernel") {
         if (value < PM_SK_PRODUCT || value > PM_SK_LOCK16) return -1;
         o->dfa.sparse_kernel = (int)value;
+        return 0;
+    }
+    if (k == "fl_hold") {
+        if (value != 0 && value != 1 && value != 2 && value != 4) return -1;
+        o->dfa.flhold = value ? (int)value : 2;
         return 0;
     }
     if (k == "dfa_sync") {

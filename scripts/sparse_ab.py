@@ -51,14 +51,16 @@ for st in args.streams.split(","):
         lib.pm_hip_gen_stream_device(text.data_ptr(), 0, n + 64, 1, 0 if st == "ascii" else 1, s.cuda_stream)
     for mode in args.modes.split(","):
         w = WIDTH[mode]
-        ks = [int(v) for v in args.kernels.split(",")]
+        ks = args.kernels.split(",")
         times = {k: [] for k in ks}
         ran = {}
         ref = None
         counts = {}
         for r in range(args.rounds + 1):
             for k in ks:
-                assert m.set_option("sparse_kernel", k) == 0
+                kk, _, hold = k.partition(":")
+                assert m.set_option("sparse_kernel", int(kk)) == 0
+                assert m.set_option("fl_hold", int(hold or 0)) == 0
                 cnt.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)

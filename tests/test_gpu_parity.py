@@ -706,7 +706,7 @@ def test_full_size_merged_deep_auto_oracle_windows(stream):
         torch.cuda.synchronize()
         held = au.hold_choice(0)
     held = au.hold_choice(2)
-    assert held in (1, 2, 3, 4)
+    assert held in (1, 2, 3, 4, 5)
     a.zero_()
     au.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c.data_ptr(), s)
     torch.cuda.synchronize()
@@ -897,8 +897,10 @@ SPARSE_KERNELS = {1: (4, 2, 0), 2: (4,), 3: (4, 2), 4: (4, 2, 0), 5: (4, 2, 0)}
 @pytest.mark.parametrize("key", ["et", "merged"])
 def test_fl_kernel_every_width(key):
     """The fallback-linked kernel (sparse_kernel 1) on et and the merged
-    dictionaries, 8 MiB of each one's lines stream plus the shipped stream:
-    u32 ids, u16 ids and the count equal the reverse-trie kernel's."""
+    dictionaries, 8 MiB of each one's lines stream plus the shipped stream,
+    with each record-load policy ("fl_hold": 16-B halves, deep records'
+    32-B and 64-B blocks): u32 ids, u16 ids and the count equal the
+    reverse-trie kernel's."""
     torch = _torch()
     rt, ac = matcher(key, "rt"), matcher(key, "ac")
     n = 8 << 20
@@ -906,6 +908,7 @@ def test_fl_kernel_every_width(key):
     dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     try:
         assert ac.set_option("dfa_form", 2) == 0 and ac.set_option("sparse_kernel", 1) == 0
+        assert ac.set_option("fl_hold", 3) == -1
         for stream in ("lines", "ship"):
             if stream == "lines":
                 rt.gen_lines_device(dt.data_ptr(), n + 64, 21, s)
@@ -913,21 +916,24 @@ def test_fl_kernel_every_width(key):
                 dt.copy_(torch.from_numpy(np.tile(SHIP, (n + 64) // len(SHIP) + 1)[: n + 64]).cuda())
             ref = torch.empty(n, dtype=torch.int32, device="cuda")
             rt.scan_device(dt.data_ptr(), 0, 0, n, ref.data_ptr(), None, s)
-            a = torch.zeros(n, dtype=torch.int32, device="cuda")
-            h = torch.zeros(n, dtype=torch.int16, device="cuda")
-            c = torch.zeros(2, dtype=torch.int64, device="cuda")
-            ac.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c[0:1].data_ptr(), s)
-            assert ac.sparse_kernel_last == 1
-            ac.scan_device(dt.data_ptr(), 0, 0, n, h.data_ptr(), None, s, out_width=2)
-            assert ac.sparse_kernel_last == 1
-            ac.scan_device(dt.data_ptr(), 0, 0, n, 0, c[1:2].data_ptr(), s)
-            assert ac.sparse_kernel_last == 1
-            torch.cuda.synchronize()
-            assert torch.equal(a, ref), stream
-            assert torch.equal(h.to(torch.int32) & 0xFFFF, ref), stream
             nz = int((ref != 0).sum().item())
-            assert int(c[0].item()) == nz and int(c[1].item()) == nz, stream
+            for hold in (1, 2, 4):
+                assert ac.set_option("fl_hold", hold) == 0
+                a = torch.zeros(n, dtype=torch.int32, device="cuda")
+                h = torch.zeros(n, dtype=torch.int16, device="cuda")
+                c = torch.zeros(2, dtype=torch.int64, device="cuda")
+                ac.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c[0:1].data_ptr(), s)
+                assert ac.sparse_kernel_last == 1
+                ac.scan_device(dt.data_ptr(), 0, 0, n, h.data_ptr(), None, s, out_width=2)
+                assert ac.sparse_kernel_last == 1
+                ac.scan_device(dt.data_ptr(), 0, 0, n, 0, c[1:2].data_ptr(), s)
+                assert ac.sparse_kernel_last == 1
+                torch.cuda.synchronize()
+                assert torch.equal(a, ref), (stream, hold)
+                assert torch.equal(h.to(torch.int32) & 0xFFFF, ref), (stream, hold)
+                assert int(c[0].item()) == nz and int(c[1].item()) == nz, (stream, hold)
     finally:
+        ac.set_option("fl_hold", 0)
         ac.set_option("sparse_kernel", 0)
         ac.set_option("dfa_form", 0)
 
@@ -1170,7 +1176,7 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
     m = matcher("et", "auto")
     kernels, forms = [], []
-    for _ in range(10):
+    for _ in range(12):
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
@@ -1178,11 +1184,11 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
         forms.append(m.dfa_form_last)
         assert torch.equal(got, want)
     # RT first (measured: it spills), then two trial launches of each DFA
-    # candidate (dense rows; rows + records; the same with 16-B record
+    # candidate (dense rows; rows + records with 16-B, 32-B and 64-B record
     # loads; the second of each timed); the fastest per position holds
-    assert kernels[:7] == [pm.KIND_RT] + [pm.KIND_AC] * 6, kernels
-    assert forms[:7] == [0, 1, 1, 2, 2, 2, 2], forms
-    assert len(set(zip(kernels[7:], forms[7:]))) == 1, (kernels, forms)
+    assert kernels[:9] == [pm.KIND_RT] + [pm.KIND_AC] * 8, kernels
+    assert forms[:9] == [0, 1, 1, 2, 2, 2, 2, 2, 2], forms
+    assert len(set(zip(kernels[9:], forms[9:]))) == 1, (kernels, forms)
 
 
 @pytest.mark.parametrize("cap", [1, 2])
@@ -1277,7 +1283,7 @@ def test_auto_scan_device_across_two_streams_and_hold():
         torch.cuda.synchronize()
         assert torch.equal(o, want)
         held = m.hold_choice(0)
-    assert held in (1, 2, 3, 4), held
+    assert held in (1, 2, 3, 4, 5), held
     assert m.hold_choice(100) == held  # pinned for the next 100 launches
     for _ in range(3):
         m.scan_device(dt.data_ptr(), 0, 0, n, outs[1].data_ptr(), None, streams[1].cuda_stream)
@@ -1410,16 +1416,16 @@ def test_ac_kind_times_both_dfa_forms(stream):
     want = torch.empty(n, dtype=torch.int32, device="cuda")
     rt.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
     forms = []
-    for _ in range(9):
+    for _ in range(11):
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
         assert ac.kernel_last == pm.KIND_AC
         forms.append(ac.dfa_form_last)
         assert torch.equal(got, want)
-    # dense rows, rows + records, the same with 16-B record loads: two
-    # launches each, then the fastest holds
-    assert forms[:6] == [1, 1, 2, 2, 2, 2] and forms[6] == forms[7] == forms[8] in (1, 2), forms
+    # dense rows, then rows + records with 16-B, 32-B and 64-B record
+    # loads: two launches each, then the fastest holds
+    assert forms[:8] == [1, 1, 2, 2, 2, 2, 2, 2] and forms[8] == forms[9] == forms[10] in (1, 2), forms
     ac.reset()  # a new stream: the forms are timed again
     ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
     torch.cuda.synchronize()
