@@ -274,12 +274,12 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    for (int layout = 0; layout < 6; ++layout) {
+    for (int layout = 0; layout < 8; ++layout) {
         const std::vector<uint8_t>& lds = layout == 5 ? inlds_v : inlds;
         Lru l2{(size_t)L2KB * 1024 / 128};
         uint64_t rowreq = 0, recreq = 0, fbreq = 0, steps = 0, rowmiss = 0, recmiss = 0, fbmiss = 0;
         std::unordered_map<uint64_t, uint64_t> lines;
-        std::vector<uint32_t> w(LANES, 0), key(LANES, ~0u);
+        std::vector<uint32_t> w(LANES, 0), key(LANES, ~0u), ws(LANES, ~0u);
         auto col = [&](uint32_t c) { return layout == 1 ? perm[c] : c; };
         auto rowline = [&](uint32_t r, uint32_t c) { return ((uint64_t)r * 1024 + col(c) * 4) / 128; };
         for (int j = 0; j < WARM + SEG; ++j) {
@@ -298,6 +298,21 @@ int main(int argc, char** argv) {
                 } else {
                     const uint32_t gr = s - F;
                     const bool deep = gr >= fl.deep_g;
+                    // layouts 6 / 7: deep records in forward windows of 4 / 8
+                    // halves (64 / 128 B) from the record's own half
+                    if (layout >= 6 && deep) {
+                        const uint32_t hh = gr >> 1, NH = layout == 6 ? 4 : 8;
+                        if (!(ws[L] != ~0u && hh >= ws[L] && hh < ws[L] + NH)) {
+                            ws[L] = hh;
+                            key[L] = ~0u;
+                            const uint64_t b0 = (uint64_t)hh * 16, b1 = b0 + NH * 16 - 1;
+                            for (uint64_t ln = b0 / 128; ln <= b1 / 128; ++ln) {
+                                const bool h = l2.touch((1ull << 40) + ln);
+                                if (cnt) { ++recreq; recmiss += !h; lines[(1ull << 40) + ln]++; }
+                            }
+                        }
+                    } else if (layout >= 6) ws[L] = ~0u;
+                    if (!(layout >= 6 && deep)) {
                     // layouts 3 / 4: deep records in 64-B / 128-B blocks
                     const uint32_t k = deep ? (gr >> (layout == 3 ? 3 : layout == 4 ? 4 : 2)) | 0x80000000u : gr >> 1;
                     const uint64_t kk = layout == 2 ? roff[gr] / 32 : k;  // (layout 2: 32-B blocks by byte offset)
@@ -306,6 +321,7 @@ int main(int argc, char** argv) {
                         const uint64_t a = (1ull << 40) + (layout == 2 ? roff[gr] : (uint64_t)gr * 8) / 128;
                         const bool h = l2.touch(a);
                         if (cnt) { ++recreq; recmiss += !h; lines[a]++; }
+                    }
                     }
                     const uint32_t* U = B + (size_t)F * 256 + 2 * (size_t)gr;
                     if (c == ((U[0] >> 16) & 0xFFu)) nw = U[1];
@@ -340,7 +356,7 @@ int main(int argc, char** argv) {
         }
         printf("%s: per step: row %.3f fallback %.3f record %.3f requests; L2 misses per step %.3f (row %.3f fb %.3f rec %.3f)\n"
                "   lines touched %zu (%.1f MB); 50/90/99%% of requests in %.2f / %.2f / %.2f MB\n",
-               layout == 5 ? "LDS rows by visits" : layout == 4 ? "deep 128-B blocks" : layout == 3 ? "deep 64-B blocks" : layout == 2 ? "compact chains" : layout ? "permuted columns" : "product", (double)rowreq / steps, (double)fbreq / steps,
+               layout == 7 ? "deep 128-B forward windows" : layout == 6 ? "deep 64-B forward windows" : layout == 5 ? "LDS rows by visits" : layout == 4 ? "deep 128-B blocks" : layout == 3 ? "deep 64-B blocks" : layout == 2 ? "compact chains" : layout ? "permuted columns" : "product", (double)rowreq / steps, (double)fbreq / steps,
                (double)recreq / steps, (double)(rowmiss + fbmiss + recmiss) / steps, (double)rowmiss / steps,
                (double)fbmiss / steps, (double)recmiss / steps, h.size(), h.size() * 128 / 1e6, n50 * 128 / 1e6,
                n90 * 128 / 1e6, n99 * 128 / 1e6);
