@@ -78,6 +78,10 @@ def parse(argv=None):
                    help="CPU-baseline processes (0 = the job's host-core share, bounded by memory)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the count_only and deep measurements")
+    p.add_argument("--image-cache", default="auto",
+                   help="compiled-automaton cache directory (SURVEY §8f item 2): 'auto' = $PM_IMAGE_CACHE, or with "
+                        "more than one rank /tmp/pm_image_cache (rank 0 compiles and writes it, the other ranks "
+                        "then read it instead of compiling); 'off' = none")
     p.add_argument("--score", action="store_true",
                    help="after timing, score the ids against the AC-DFA reliable instance on the device "
                         "(measure.c:174-190) and report FP/FN/partial rates (dense mode)")
@@ -191,6 +195,29 @@ def cpu_legs(args):
     return out
 
 
+def image_cache_dir(args, world):
+    """Where the ranks share the compiled automaton (None: each compiles)."""
+    if args.image_cache == "off":
+        return None
+    if args.image_cache != "auto":
+        return args.image_cache
+    return os.environ.get("PM_IMAGE_CACHE") or ("/tmp/pm_image_cache" if world > 1 else None)
+
+
+def compile_ordered(build, cache_dir, use_dist, rank, dist):
+    """Rank 0 compiles first (writing the shared image cache), the others
+    after a barrier (reading it): N ranks pay one host compile, not N.
+    Each rank still uploads its own replica of the automaton to its GPU
+    (replicated per GPU).  Returns build()'s value."""
+    shared = use_dist and cache_dir is not None
+    if shared and rank != 0:
+        dist.barrier()
+    v = build()
+    if shared and rank == 0:
+        dist.barrier()
+    return v
+
+
 def extras_on(args):
     return (not args.no_extra and args.stream == "ascii" and args.mode == "dense" and args.kernel == "rt"
             and args.layout == "shards")
@@ -283,15 +310,35 @@ def main():
     backend = os.environ.get("PM_BENCH_BACKEND", "nccl")
     if os.environ.get("PM_BENCH_REHEARSE") == "1":
         # launcher / rendezvous rehearsal without a GPU (CPU test suite): gloo,
-        # no device, placeholder timings; never a measurement
+        # no device, placeholder timings; never a measurement.  The start-up
+        # protocol runs for real on the host: rank 0 flattens the automaton
+        # into the shared image cache, the others read it after the barrier
         dist.init_process_group("gloo")
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t)
+        startup = None
+        cache_dir = image_cache_dir(args, world)
+        if cache_dir is not None:
+            import ctypes
+            import patternmatching_amd as pm
+            lib = pm.load()
+            t0 = time.perf_counter()
+            pats = pm.Dictionary([os.path.join(DATA, x) for x in DICTS[args.dict]]).patterns()
+            arr = (ctypes.c_char_p * len(pats))(*pats)
+            lens = (ctypes.c_uint32 * len(pats))(*[len(x) for x in pats])
+            t1 = time.perf_counter()
+            h = compile_ordered(lambda: lib.pm_flat_build_cached(arr, lens, len(pats), 1, cache_dir.encode()),
+                                cache_dir, True, rank, dist)
+            startup = {"dict_load_ms": round((t1 - t0) * 1e3, 2),
+                       "compile_ms": round((time.perf_counter() - t1) * 1e3, 2),
+                       "image_cache": "hit" if lib.pm_flat_cache_hit(h) else "miss", "image_kind": "rt (host only)"}
+            lib.pm_flat_free(h)
         ranks = [None] * dist.get_world_size()
-        dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid()})
+        dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid(), "startup": startup})
         if rank == 0:
             print(json.dumps({"rehearsal": True, "n_gpus": dist.get_world_size(), "world_size": dist.get_world_size(),
-                              "rank_sum": t.item(), "per_rank": ranks, "cpu_baseline": cpu and cpu["main"]}),
+                              "rank_sum": t.item(), "per_rank": ranks, "image_cache_dir": cache_dir,
+                              "cpu_baseline": cpu and cpu["main"]}),
                   flush=True)
         dist.destroy_process_group()
         return
@@ -353,10 +400,28 @@ def main():
     global HBM_PEAK_GBS
     HBM_PEAK_GBS = lib.pm_hip_hbm_peak_gbs()  # the one constant the CLI's CSV prices against too
 
+    # start-up, per rank: the dictionary's parse, then compile() -- the host
+    # flatten (or the shared image cache's read) and the upload of this
+    # rank's replica of the automaton to its GPU
+    t_s0 = time.perf_counter()
     d = pm.Dictionary([os.path.join(DATA, x) for x in DICTS[args.dict]])
+    dict_ms = (time.perf_counter() - t_s0) * 1e3
+    cache_dir = image_cache_dir(args, world)
     m = pm.HipMatcher(args.kernel)
+    if cache_dir:
+        m.set_image_cache(cache_dir)
     m.add_dictionary(d)
-    m.compile()
+    compile_ordered(m.compile, cache_dir, use_dist, rank, dist)
+    cs = m.compile_stats()
+    startup = {"dict_load_ms": round(dict_ms, 2), "compile_ms": cs["compile_ms"], "upload_ms": cs["upload_ms"],
+               "image_bytes": cs["image_bytes"],
+               "upload_gbps": round(cs["image_bytes"] / (cs["upload_ms"] * 1e-3) / 1e9, 2) if cs["upload_ms"] else None,
+               "image_cache": ("hit" if cs["image_cache_hit"] else "miss") if cache_dir else "off",
+               "wall_ms": round((time.perf_counter() - t_s0) * 1e3, 2)}
+    startups = [startup]
+    if use_dist:
+        startups = [None] * world
+        dist.all_gather_object(startups, startup)
 
     n = args.bytes
     stream = torch.cuda.current_stream()
@@ -602,8 +667,9 @@ def main():
             },
             "world_size": world,
             "per_rank": [{"rank": int(r[0]), "gbps": round(g, 3), "kernel_ms": round(r[2], 4),
-                          "device": devices[int(r[0])]}
+                          "device": devices[int(r[0])], "startup": startups[int(r[0])]}
                          for r, g in zip(per_rank, rates)],
+            "image_cache_dir": cache_dir,
             "match_count_all_reduce_ms": round(count_ar_ms, 3) if use_dist else None,
             "rank_spread": round(max(rates) / min(rates), 4),
             "matches_per_sec": round(total_matches / elapsed, 1),
@@ -742,13 +808,20 @@ def gather_roofline(lib, mat, kernel_ms, tr, steps=2048):
     ceiling = steps * 1024 * ncu / (ms * 1e-3) / 1e9
     req = tr.get("l2_read_requests") if tr else None
     ach = req / (kernel_ms * 1e-3) / 1e9 if req else None
-    return {"bound": "gathers", "unit": "G loads/s", "ceiling": round(ceiling, 2),
-            "achieved": round(ach, 2) if ach else None, "frac": round(ach / ceiling, 4) if ach else None,
+    # Two different quantities side by side, named as what they are (ADVICE
+    # r05): the kernel's L2 read-request rate (text loads included, LDS row
+    # hits and register-held record blocks excluded) and the probe's rate of
+    # dependent 4-B global loads; their ratio is an indication of headroom,
+    # not a roofline fraction of one quantity
+    return {"bound": "gathers", "unit": "G/s", "ceiling": round(ceiling, 2),
+            "ceiling_is": "dependent uniform 4-B global loads per second (probe)",
+            "l2_read_request_rate": round(ach, 2) if ach else None,
+            "request_rate_over_load_ceiling": round(ach / ceiling, 4) if ach else None,
             "requests_per_launch": req, "ceiling_ms": round(ms, 4), "ceiling_loads": steps * 1024 * ncu,
             "what": "ceiling: pm_hip_gather_ceiling_device over this object's FL image (dependent uniform 4-B "
-                    "loads, the kernel's launch shape); achieved: TCP_TCC_READ_REQ_sum per launch "
-                    "(profiles/traffic.json: the L2 read requests, the table loads and ~1/16 per byte of text "
-                    "loads) / kernel time"}
+                    "loads, the kernel's launch shape); l2_read_request_rate: TCP_TCC_READ_REQ_sum per launch "
+                    "(profiles/traffic.json: L1-to-L2 read requests -- table loads and ~1/16 per byte of text "
+                    "loads) / kernel time.  Different units of work: their ratio is not a roofline fraction"}
 
 
 def load_traffic(workload_key):

@@ -139,6 +139,12 @@ size_t pm_hip_scratch_bytes(void* obj);
 void pm_hip_set_image_cache(void* obj, const char* dir);
 /* 1 when the last compile() loaded its tables from the cache. */
 int pm_hip_image_cache_hit(void* obj);
+/* Start-up cost of the last compile(): *compile_ms = the whole call (gid
+ * numbering, flattening or the cache read, the uploads), *upload_ms = its
+ * host-to-device table copies (pm_hip_table_bytes bytes).  Wall time, ms.
+ * 0, or -1 before compile().  (No reference counterpart: the reference's
+ * init_mps, mps.c:109-113, is untimed.) */
+int pm_hip_compile_stats(void* obj, double* compile_ms, double* upload_ms);
 /* The patterns-tree parent of a gid (longest proper suffix pattern, 0 = none);
  * UINT32_MAX when out of range. */
 uint32_t pm_hip_parent_gid(void* obj, uint32_t gid);
@@ -171,8 +177,8 @@ int pm_hip_kernel_last(void* obj);
  * (pm_flatten.h), 0 = the RT kernel ran. */
 int pm_hip_dfa_form_last(void* obj);
 /* The sparse form's kernel of the last launch that ran it ("sparse_kernel"
- * option numbering: 1 fallback-linked, 2 u16-staged 8-B units, 3 u32-staged,
- * 4 lock-step 8-B units, 5 lock-step 16-B records; 0 before any). */
+ * option numbering: 1 fallback-linked, 2 lock-step 8-B units, 3 lock-step
+ * 16-B records; 0 before any). */
 int pm_hip_sparse_kernel_last(void* obj);
 /* Seconds of device time of the scan kernels issued through read_block
  * since the last reset (hipEvent based); -1 when some of those launches were
@@ -200,12 +206,15 @@ int pm_hip_set_device(int device);
  *   "dfa_form"        ac / auto kinds: 0 = timed choice between the DFA's
  *                     dense rows and sparse form (default), 1 = dense rows,
  *                     2 = sparse form (the pick measures again)
- *   "sparse_kernel"   the sparse form's kernel: 0 = the product choice per
- *                     output width (default), 1 = fallback-linked form (u32
- *                     ids), 2 = u16-staged 8-B units (u32 ids), 3 = u32-staged
- *                     8-B units, 4 = lock-step 8-B units, 5 = lock-step 16-B
- *                     records; a launch the object or width cannot run with
- *                     the forced kernel fails (-3)
+ *   "sparse_kernel"   the sparse form's kernel: 0 = the product choice
+ *                     (default: the fallback-linked form where the object
+ *                     has it), 1 = fallback-linked form, 2 = lock-step 8-B
+ *                     units, 3 = lock-step 16-B records.  A forced kernel
+ *                     whose image the object lacks (the FL form needs fewer
+ *                     than 65,536 rows and gids, the 8-B units ids below
+ *                     2^20) is not an error: the launch runs the product
+ *                     choice, and pm_hip_sparse_kernel_last reports which
+ *                     kernel ran
  *   "fl_hold"         the fallback-linked kernel's record loads outside the
  *                     picks' trials: 2 = deep records' 32-B blocks (0, the
  *                     default), 4 = 64-B blocks, 1 = every record as a 16-B

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <cstring>
 #include <unordered_map>
@@ -799,6 +800,9 @@ bool get(FILE* f, uint32_t tag, std::vector<T>& v) {
 
 bool save(const std::string& path, uint64_t key, int kind, const PmImages& im) {
     const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+    // the cache directory and its parents, as `mkdir -p` (existing ones are fine)
+    for (size_t k = path.find('/', 1); k != std::string::npos; k = path.find('/', k + 1))
+        (void)::mkdir(path.substr(0, k).c_str(), 0755);
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) return false;
     const uint32_t hdr[2] = {IMG_VERSION, (uint32_t)kind};

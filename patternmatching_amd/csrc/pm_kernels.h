@@ -37,14 +37,14 @@ struct RtDev {
 int64_t pm_rt_spill_items(int64_t n, int num_cu, int64_t cap_chunks);
 
 // Kernels of the sparse DFA form (DfaDev::sparse_kernel; pm_kernels.hip
-// pm_launch_dfa lists the product choice per output width)
+// pm_dfa_sparse_choice is the product choice).  The u32- and u16-staged
+// 8-B-unit kernels of round 4 were retired in round 6 (no default path
+// picked them once the FL form existed; MEASUREMENTS.md keeps their numbers).
 enum PmSparseKernel {
     PM_SK_PRODUCT = 0,
-    PM_SK_FL = 1,       // dfa_fl_kernel: the fallback-linked form (u32 ids)
-    PM_SK_STAGE16 = 2,  // dfa_sparse_stage16_kernel: 8-B units, u16-staged ids (u32 ids)
-    PM_SK_STAGE = 3,    // dfa_sparse_stage_kernel: 8-B units, u32-staged ids
-    PM_SK_LOCK8 = 4,    // dfa_sparse_lds_kernel over 8-B units, lock step
-    PM_SK_LOCK16 = 5,   // dfa_sparse_lds_kernel over the 16-B records, lock step
+    PM_SK_FL = 1,      // dfa_fl_kernel: the fallback-linked form (every width)
+    PM_SK_LOCK8 = 2,   // dfa_sparse_lds_kernel over 8-B units, lock step (automata without the FL form)
+    PM_SK_LOCK16 = 3,  // dfa_sparse_lds_kernel over the 16-B records, lock step (ids past the 8-B units' 2^20)
 };
 
 struct DfaDev {
@@ -57,7 +57,6 @@ struct DfaDev {
     uint32_t sF;           // states with full rows
     const uint8_t* sbase8;  // the same with 8-B record units (pm_pack_sparse8), or null
     const uint32_t* sout8;  // its ids' outputs
-    const uint16_t* sout8h; // the same as u16 when every gid < 65536 (else null)
     // 2^24-bit set of the 3-byte strings occurring in some pattern (bit
     // t[q] | t[q+1] << 8 | t[q+2] << 16), or null.  A 3-gram outside it is
     // synchronizing: the state after it is the root's over those 3 bytes
@@ -79,6 +78,9 @@ struct DfaDev {
     // the default), 4 (64-B blocks) or 1 (every record as a 16-B half,
     // flGD ignored); the auto / ac picks time all three
     int flhold = 2;
+    // chains per lane of the FL kernel: 1 = dfa_fl_kernel, 2 = dfa_fl2_kernel
+    // (two segments per lane in lock step; record holds of NR 1 or 2)
+    int flchains = 1;
 };
 
 // Positions [pos0, pos0+n) of text; bytes back to stream_start are context.

@@ -1593,260 +1593,6 @@ __global__ __launch_bounds__(DFA_LDS_THREADS) __attribute__((amdgpu_waves_per_eu
     }
 }
 
-// The sparse form with its ids staged in LDS (round 4).  PMC of the
-// lock-step kernel above on the lines stream: the TA is ~75% busy, and two
-// things behind the steps cost more than their bytes (timing ablations,
-// snort, 1 GiB, dense u32; profiles/r04/dyn): the escape lookups -- an outt
-// load instruction for each of a block's 32 positions, almost every one
-// issued for a lane or two (6.51 -> 5.98 ms without them) -- and the id
-// stores, eight 16-B stores per lane per block, each instruction touching
-// 64 lines (6.51 -> 5.36 ms without them; with every lane's ids sent to one
-// L2-resident line 6.31: the lines' HBM traffic is not the cost).  Here:
-//  * each step writes its id, or for an escape its coded word, into the
-//    lane's staging row in LDS: one ds_write_b32 at an immediate offset,
-//    rows of 33 dwords so the 64 lanes of a step hit 64 banks; no register
-//    array holds the block's words;
-//  * escapes go in rounds over the lanes' escape masks: per round each
-//    lane with one left loads it (a round per escape of the lane with the
-//    most, ~2-4 per block, instead of 32 load instructions);
-//  * the block goes out transposed: store instruction t writes the 128-B
-//    line of chain 8t + lane / 8, chunk lane % 8 -- eight whole lines per
-//    instruction instead of 16-B pieces of 64 lines (NT: non-temporal).
-// Every loop a lane's exchange depends on is wave-uniform (lanes without a
-// segment or past their last block take part and store nothing).
-// (Product for gids past u16; its timing ablations and the u16-escape-table
-// form of round 4 are in git history.)
-template <int OUTW, int KR, int THREADS, bool NT, int BU = 8>
-__global__ __launch_bounds__(THREADS) void dfa_sparse_stage_kernel(
-    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
-    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
-    const uint32_t* __restrict__ outt, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
-    constexpr int BLK = 32, SROW = 33;  // a lane's staging row: 32 ids + one pad dword
-    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR ? KR * 256 : 1];
-    __shared__ uint32_t s_ids[THREADS * SROW];
-    if (KR) {
-        const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
-        const uint4* src = reinterpret_cast<const uint4*>(base);
-        uint4* dst = reinterpret_cast<uint4*>(s_rows);
-        for (uint32_t k = threadIdx.x; k < nr * 64u; k += THREADS) dst[k] = src[k];
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & 63;
-    uint32_t* const my = s_ids + threadIdx.x * SROW;
-    const uint32_t* const wrows = s_ids + (threadIdx.x - lane) * SROW;  // the wave's rows
-    const int64_t nseg = (n + seg_len - 1) / seg_len;
-    const int64_t lanes = (int64_t)gridDim.x * THREADS;
-    uint32_t cnt = 0, cb = 0xFFFFFFFFu;
-    uint4 R[4] = {};
-    for (int64_t sg0 = (int64_t)blockIdx.x * THREADS + threadIdx.x; __ballot(sg0 < nseg); sg0 += lanes) {
-        const bool has = sg0 < nseg;
-        const int64_t lo = has ? pos0 + sg0 * seg_len : pos0 + n;
-        const int64_t hi = has ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : pos0 + n;
-        int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
-        if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
-        uint32_t s = 0;
-        for (int64_t i = wlo; i < lo; ++i) s = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, text[i], cb, R) & DFA_STATE_MASK;
-        const int64_t nblk = seg_len / BLK;
-        for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
-            bool act[2];
-            uint32_t WT[2][8];
-#pragma unroll
-            for (int tt = 0; tt < 2; ++tt) {
-                act[tt] = lo + BLK * (b0 + tt) + BLK <= hi;
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const tu32x4 w = act[tt] ? *reinterpret_cast<const tu32x4*>(text + lo + BLK * (b0 + tt) + 16 * q)
-                                             : tu32x4{0u, 0u, 0u, 0u};
-                    WT[tt][4 * q] = w.x;
-                    WT[tt][4 * q + 1] = w.y;
-                    WT[tt][4 * q + 2] = w.z;
-                    WT[tt][4 * q + 3] = w.w;
-                }
-            }
-            if (!__ballot(act[0])) break;
-            unroll_for<0, 2>([&](auto tc) {
-                constexpr int tt = decltype(tc)::value;
-                if (tt == 1 && !__ballot(act[1])) return;
-                const int64_t b = b0 + tt;
-                uint32_t em = 0;  // this block's escapes
-#pragma unroll
-                for (int j = 0; j < BLK; ++j) {
-                    const uint32_t v = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb, R);
-                    s = act[tt] ? v & DFA_STATE_MASK : s;
-                    cnt += act[tt] && v >= (1u << 20);  // a nonzero id (an escape is one)
-                    if (OUTW) {
-                        const bool esc = v >= (DFA_ESC << 20);
-                        my[j] = esc ? v : v >> 20;
-                        em |= esc ? 1u << j : 0u;
-                    }
-                }
-                if (!OUTW) return;
-                if (!act[tt]) em = 0;
-                // (measured and removed: up to 4 / 8 escapes per lane per
-                // round, their loads issued together -- no faster, lines 5.75
-                // -> 5.74 / 5.75 ms; profiles/r04/gid_order)
-                while (__ballot(em != 0)) {  // one escape per lane per round
-                    if (em) {
-                        const uint32_t j = __builtin_ctz(em);
-                        em &= em - 1;
-                        my[j] = outt[my[j] & DFA_STATE_MASK];
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (OUTW == 4) {
-                    const uint64_t am = __ballot(act[tt]);
-                    uint32_t* o = reinterpret_cast<uint32_t*>(out) + (sg0 - lane + (lane >> 3)) * seg_len + BLK * b +
-                                  4 * (lane & 7);
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        const int c = 8 * t + (lane >> 3);
-                        const uint32_t* src = wrows + c * SROW + 4 * (lane & 7);
-                        const tu32x4 v = {src[0], src[1], src[2], src[3]};
-                        if ((am >> c) & 1u) {
-                            if (NT) __builtin_nontemporal_store(v, reinterpret_cast<tu32x4*>(o));
-                            else *reinterpret_cast<tu32x4*>(o) = v;
-                        }
-                        o += 8 * seg_len;
-                    }
-                } else if (act[tt]) {  // u16 ids: the lane's own 64 B
-                    tu32x4* o = reinterpret_cast<tu32x4*>(reinterpret_cast<uint16_t*>(out) + (lo - pos0) + BLK * b);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        o[q] = tu32x4{my[8 * q] | my[8 * q + 1] << 16, my[8 * q + 2] | my[8 * q + 3] << 16,
-                                      my[8 * q + 4] | my[8 * q + 5] << 16, my[8 * q + 6] | my[8 * q + 7] << 16};
-                }
-                __builtin_amdgcn_wave_barrier();
-            });
-        }
-        // the segment's last (< BLK) positions
-        for (int64_t i = lo + BLK * ((hi - lo) / BLK); i < hi; ++i) {
-            s = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, text[i], cb, R) & DFA_STATE_MASK;
-            const uint32_t v = outt[s];
-            if (OUTW) put_id<OUTW>(out, i - pos0, v);
-            cnt += v != 0u;
-        }
-    }
-    if (count) {
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
-        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
-    }
-}
-
-// dfa_sparse_stage_kernel with u16 staging rows (u32 ids out; every gid <
-// 65536): a lane's row is 17 dwords (32 u16 ids + pad; 17 is odd, so the
-// 64 lanes of a step still hit 64 banks), half of the 32-bit rows, and the
-// LDS that frees holds KR fallback rows instead of 16 (the model, scripts/
-// sdfa_wave_model.cpp, lines stream: 1.91 dependent loads per wave step with
-// 16 rows, 1.77 with 80).  An escape's slot holds the low 16 bits of its
-// state, the high 4 bits sit in four registers (hi4, 8 positions each).
-template <int KR, int BU, bool NT = false>
-__global__ __launch_bounds__(1024) void dfa_sparse_stage16_kernel(
-    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, uint32_t* __restrict__ out,
-    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F,
-    const uint32_t* __restrict__ outt, const uint16_t* __restrict__ outt16, int64_t warm, int64_t seg_len,
-    const uint32_t* __restrict__ gram3) {
-    constexpr int THREADS = 1024, BLK = 32, SROW = 17;
-    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
-    __shared__ uint32_t s_ids[THREADS * SROW];
-    {
-        const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
-        const uint4* src = reinterpret_cast<const uint4*>(base);
-        uint4* dst = reinterpret_cast<uint4*>(s_rows);
-        for (uint32_t k = threadIdx.x; k < nr * 64u; k += THREADS) dst[k] = src[k];
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & 63;
-    uint16_t* const my = reinterpret_cast<uint16_t*>(s_ids + threadIdx.x * SROW);
-    const uint32_t* const wrows = s_ids + (threadIdx.x - lane) * SROW;  // the wave's rows
-    const int64_t nseg = (n + seg_len - 1) / seg_len;
-    const int64_t lanes = (int64_t)gridDim.x * THREADS;
-    uint32_t cnt = 0, cb = 0xFFFFFFFFu;
-    uint4 R[4] = {};
-    for (int64_t sg0 = (int64_t)blockIdx.x * THREADS + threadIdx.x; __ballot(sg0 < nseg); sg0 += lanes) {
-        const bool has = sg0 < nseg;
-        const int64_t lo = has ? pos0 + sg0 * seg_len : pos0 + n;
-        const int64_t hi = has ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : pos0 + n;
-        int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
-        if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
-        uint32_t s = 0;
-        for (int64_t i = wlo; i < lo; ++i) s = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, text[i], cb, R) & DFA_STATE_MASK;
-        const int64_t nblk = seg_len / BLK;
-        for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
-            bool act[2];
-            uint32_t WT[2][8];
-#pragma unroll
-            for (int tt = 0; tt < 2; ++tt) {
-                act[tt] = lo + BLK * (b0 + tt) + BLK <= hi;
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    // (measured and removed: non-temporal text loads -- lines
-                    // 5.47 -> 5.74 ms, the next segment's warm-up re-reads
-                    // these lines; shipped 3.43 -> 3.13; stage16_nt_text_ab.json)
-                    const tu32x4* tp = reinterpret_cast<const tu32x4*>(text + lo + BLK * (b0 + tt) + 16 * q);
-                    const tu32x4 w = act[tt] ? *tp : tu32x4{0u, 0u, 0u, 0u};
-                    WT[tt][4 * q] = w.x;
-                    WT[tt][4 * q + 1] = w.y;
-                    WT[tt][4 * q + 2] = w.z;
-                    WT[tt][4 * q + 3] = w.w;
-                }
-            }
-            if (!__ballot(act[0])) break;
-            unroll_for<0, 2>([&](auto tc) {
-                constexpr int tt = decltype(tc)::value;
-                if (tt == 1 && !__ballot(act[1])) return;
-                const int64_t b = b0 + tt;
-                uint32_t em = 0, hi4[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int j = 0; j < BLK; ++j) {
-                    const uint32_t v = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, (WT[tt][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb, R);
-                    s = act[tt] ? v & DFA_STATE_MASK : s;
-                    cnt += act[tt] && v >= (1u << 20);  // a nonzero id (an escape is one)
-                    const bool esc = v >= (DFA_ESC << 20);
-                    my[j] = (uint16_t)(esc ? v : v >> 20);
-                    hi4[j >> 3] |= esc ? ((v >> 16) & 0xFu) << (4 * (j & 7)) : 0u;
-                    em |= esc ? 1u << j : 0u;
-                }
-                if (!act[tt]) em = 0;
-                while (__ballot(em != 0)) {  // one escape per lane per round
-                    if (em) {
-                        const uint32_t j = __builtin_ctz(em);
-                        em &= em - 1;
-                        const uint32_t h = j < 16 ? (j < 8 ? hi4[0] : hi4[1]) : (j < 24 ? hi4[2] : hi4[3]);
-                        my[j] = outt16[my[j] | ((h >> (4 * (j & 7))) & 0xFu) << 16];
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                const uint64_t am = __ballot(act[tt]);
-                uint32_t* o = out + (sg0 - lane + (lane >> 3)) * seg_len + BLK * b + 4 * (lane & 7);
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const int c = 8 * t + (lane >> 3);
-                    const uint32_t* src = wrows + c * SROW + 2 * (lane & 7);
-                    const uint32_t w0 = src[0], w1 = src[1];
-                    const tu32x4 v = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
-                    if ((am >> c) & 1u) {
-                        if (NT) __builtin_nontemporal_store(v, reinterpret_cast<tu32x4*>(o));
-                        else *reinterpret_cast<tu32x4*>(o) = v;
-                    }
-                    o += 8 * seg_len;
-                }
-                __builtin_amdgcn_wave_barrier();
-            });
-        }
-        // the segment's last (< BLK) positions
-        for (int64_t i = lo + BLK * ((hi - lo) / BLK); i < hi; ++i) {
-            s = sdfa_lds_step<KR, 8, BU>(base, F, s_rows, s, text[i], cb, R) & DFA_STATE_MASK;
-            const uint32_t v = outt[s];
-            out[i - pos0] = v;
-            cnt += v != 0u;
-        }
-    }
-    if (count) {
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
-        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
-    }
-}
-
 // A value every lane of the wave holds, in scalar registers.
 __device__ __forceinline__ int64_t wave_uniform64(int64_t v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
@@ -1991,9 +1737,12 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
     return ((g & 1u) ? RR.z : RR.x) & 0xFFFFu;
 }
 
-// The FL form's scan: the staged-id structure of dfa_sparse_stage16_kernel
-// (u16 staging rows, escapes in rounds, whole-line non-temporal stores;
-// 1,024-lane workgroups, the KR shallowest rows in LDS), the FL step, and
+// The FL form's scan: ids staged in LDS (u16 staging rows of 17 dwords, so
+// the 64 lanes of a step hit 64 banks; the rare row outputs past the inline
+// code resolved in rounds, one load per lane per round), whole-line
+// non-temporal stores (store instruction t writes the 128-B lines of chains
+// CPI * t + lane / LPC), 1,024-lane workgroups, the KR profile-chosen rows
+// in LDS, the FL step, and
 // outputs one step late: a step writes the output of the position before it
 // (the state it starts from holds it).  OUTW 4 / 2: u32 / u16 ids (a u16
 // block of a chain is 64 B: four lanes' 16-B stores, 16 chains per store
@@ -2154,6 +1903,301 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
             if (OUTW == 4) reinterpret_cast<uint32_t*>(out)[i - pos0] = id;
             if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[i - pos0] = (uint16_t)id;
             cnt += id != 0u;
+        }
+    }
+    if (count) {
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(count, (unsigned long long)cnt);
+    }
+}
+
+// ---- two chains per lane (round 6) ----------------------------------------
+// A wave's step waits for the slowest of its 64 lanes' dependent loads (the
+// record block a lane enters, then at a slot miss its fallback row's word):
+// on pattern-dense text nearly every wave step has a lane that goes past L2,
+// so dfa_fl_kernel runs at about one memory latency per wave step (~1.2 us
+// per step on the lines stream, the SIMDs ~25% busy).  Here each lane walks
+// two segments in lock step and issues the loads of both before it waits
+// for either: two positions per lane per wave step for about one latency.
+// The step is fl_step in three parts -- fl_issue (the row word, the record
+// block, the LDS row word), fl_mid (on the block: the slot test, the
+// record's output, the fallback row's word), fl_fin (the select) -- run
+// chain A, chain B at each part.  Twice the staging rows (2 x 17 dwords a
+// lane, 136 KiB) leave LDS for FL2_LDS_ROWS rows when ids are written; the
+// count keeps FL_COUNT_LDS_ROWS.
+constexpr int FL2_LDS_ROWS = 24;
+
+struct FlPend {
+    uint32_t s, c, fb, x, lw, r0, y, g;
+    bool isrow, lrow, deep, miss;
+};
+
+template <int KR, int NR>
+__device__ __forceinline__ void fl_issue(const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
+                                         const uint32_t* __restrict__ s_rows, bool on, uint32_t w, uint32_t c,
+                                         uint32_t& cb, FlHold<NR>& H, FlPend& P) {
+    P.s = w & DFA_STATE_MASK;
+    P.c = c;
+    P.isrow = P.s < F;
+    P.g = P.s - F;
+    P.deep = fl_deep<NR>(P.g, GD);
+    const uint32_t key = fl_key<NR>(P.g, P.deep);
+    P.fb = w >> 20;
+    const bool newblk = on && !P.isrow && key != cb;
+    P.lrow = P.isrow && P.s < (uint32_t)KR;
+    P.x = 0;
+    if (on && P.isrow && !P.lrow) P.x = *reinterpret_cast<const uint32_t*>(base + (P.s * 1024u + c * 4u));
+    if (newblk) {
+        fl_load(base, F, P.g, P.deep, H);
+        cb = key;
+    }
+    P.lw = s_rows[(bmask(P.lrow) & P.s) * 256u + c];  // (row 0 for the other lanes: no branch)
+}
+
+template <int KR, int NR>
+__device__ __forceinline__ void fl_mid(const uint8_t* __restrict__ base, const uint32_t* __restrict__ s_rows, bool on,
+                                       const FlHold<NR>& H, FlPend& P, uint32_t& own) {
+    const tu32x4 RR = fl_reg(H, P.g, P.deep);
+    const uint32_t m1 = bmask(P.g & 1u);
+    const uint32_t w0 = bsel(m1, RR.x, RR.z), w1 = bsel(m1, RR.y, RR.w), w2 = RR.z, w3 = RR.w;
+    own = w0 & 0xFFFFu;
+    const uint32_t c = P.c;
+    const bool h0 = c == ((w0 >> 16) & 0xFFu), h1 = c == (w0 >> 24);
+    const uint32_t row = bsel(bmask(P.fb == PM_FL_INREC), P.fb, w3);
+    P.miss = !P.isrow && !h0 && !h1;
+    P.y = 0;
+    if (on && P.miss) {
+        if (KR && row < (uint32_t)KR) P.y = s_rows[row * 256u + c];
+        else P.y = *reinterpret_cast<const uint32_t*>(base + (row * 1024u + c * 4u));
+    }
+    P.r0 = bsel(bmask(P.isrow), bsel(bmask(h0), bsel(bmask(h1), 0u, w2), w1), bsel(bmask(P.lrow), P.x, P.lw));
+}
+
+__device__ __forceinline__ uint32_t fl_fin(const FlPend& P) { return bsel(bmask(P.miss), P.r0, P.y); }
+
+// fl_output in two parts: the block load of a record state (for both
+// chains before either is used), then the output.
+template <int NR>
+__device__ __forceinline__ void fl_out_issue(const uint8_t* __restrict__ base, uint32_t F, uint32_t GD, uint32_t w,
+                                             uint32_t& cb, FlHold<NR>& H) {
+    const uint32_t s = w & DFA_STATE_MASK;
+    if (s >= F) {
+        const uint32_t g = s - F;
+        const bool deep = fl_deep<NR>(g, GD);
+        const uint32_t key = fl_key<NR>(g, deep);
+        if (key != cb) {
+            fl_load(base, F, g, deep, H);
+            cb = key;
+        }
+    }
+}
+template <int NR>
+__device__ __forceinline__ uint32_t fl_out_get(uint32_t F, uint32_t GD, uint32_t w, const FlHold<NR>& H, bool& esc) {
+    const uint32_t s = w & DFA_STATE_MASK;
+    esc = false;
+    if (s < F) {
+        esc = (w >> 20) == DFA_ESC;
+        return w >> 20;
+    }
+    const uint32_t g = s - F;
+    const tu32x4 RR = fl_reg(H, g, fl_deep<NR>(g, GD));
+    return ((g & 1u) ? RR.z : RR.x) & 0xFFFFu;
+}
+
+// dfa_fl_kernel with two chains per lane (the segments of chain k of lane l
+// in a wave: wave base + 64 k + l, so each chain set of a wave is 64
+// consecutive segments and its stores are dfa_fl_kernel's whole lines).
+template <int KR, int OUTW = 4, int NR = 1>
+__global__ __launch_bounds__(1024) void dfa_fl2_kernel(
+    const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
+    unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
+    const uint16_t* __restrict__ rowout16, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
+    static_assert(OUTW == 0 || OUTW == 2 || OUTW == 4, "u32 / u16 ids or the count");
+    constexpr int THREADS = 1024, BLK = 32, SROW = 17, CH = 2;
+    constexpr bool kIds = OUTW != 0;
+    __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
+    __shared__ uint32_t s_ids[kIds ? CH * THREADS * SROW : 1];
+    {
+        const uint32_t nr = F < (uint32_t)KR ? F : (uint32_t)KR;
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_rows);
+        for (uint32_t k = threadIdx.x; k < nr * 64u; k += THREADS) dst[k] = src[k];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint16_t* my[CH];
+    const uint32_t* wrows[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        my[k] = reinterpret_cast<uint16_t*>(s_ids + (kIds ? k * THREADS * SROW + threadIdx.x * SROW : 0));
+        wrows[k] = s_ids + (kIds ? k * THREADS * SROW + (threadIdx.x - lane) * SROW : 0);
+    }
+    const int64_t nseg = (n + seg_len - 1) / seg_len;
+    const int64_t nwaves = (int64_t)gridDim.x * (THREADS / 64);
+    const uint32_t sl = (uint32_t)seg_len;
+    uint32_t cnt = 0, cb[CH], own[CH], w[CH];
+    FlHold<NR> H[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        cb[k] = 0xFFFFFFFFu;
+        own[k] = 0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) H[k].R[r] = tu32x4{0u, 0u, 0u, 0u};
+    }
+    for (int64_t wv = (int64_t)blockIdx.x * (THREADS / 64) + wid; wv * 64 * CH < nseg; wv += nwaves) {  // uniform
+        const int64_t wseg = wv * 64 * CH;
+        int64_t lo[CH], hi[CH], wlo[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int64_t sg = wseg + 64 * k + lane;
+            const bool has = sg < nseg;
+            lo[k] = has ? pos0 + sg * seg_len : pos0 + n;
+            hi[k] = has ? (lo[k] + seg_len < pos0 + n ? lo[k] + seg_len : pos0 + n) : pos0 + n;
+            wlo[k] = !has ? lo[k] : lo[k] - warm < stream_start ? stream_start : lo[k] - warm;
+            if (gram3) wlo[k] = dfa_sync_lo(text, lo[k], wlo[k], gram3);
+            w[k] = 0;  // the root, reached by no word
+        }
+        // the warm-ups, both chains in lock step
+        for (int64_t t = 0; __ballot(wlo[0] + t < lo[0] || wlo[1] + t < lo[1]); ++t) {
+            bool on[CH];
+            uint32_t cc[CH];
+            FlPend P[CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                on[k] = wlo[k] + t < lo[k];
+                cc[k] = on[k] ? text[wlo[k] + t] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < CH; ++k) fl_issue<KR, NR>(base, F, GD, s_rows, on[k], w[k], cc[k], cb[k], H[k], P[k]);
+#pragma unroll
+            for (int k = 0; k < CH; ++k) fl_mid<KR, NR>(base, s_rows, on[k], H[k], P[k], own[k]);
+#pragma unroll
+            for (int k = 0; k < CH; ++k) w[k] = on[k] ? fl_fin(P[k]) : w[k];
+        }
+        const int64_t nblk = seg_len / BLK;
+        for (int64_t b = 0; b < nblk; ++b) {
+            bool act[CH];
+            uint32_t WT[CH][8];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                act[k] = lo[k] + BLK * b + BLK <= hi[k];
+                const uint8_t* const tb = text + pos0 + (wseg + 64 * k) * seg_len;  // wave-uniform
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const tu32x4* tp =
+                        reinterpret_cast<const tu32x4*>(tb + ((uint32_t)lane * sl + (uint32_t)(BLK * b + 16 * q)));
+                    const tu32x4 v = act[k] ? *tp : tu32x4{0u, 0u, 0u, 0u};
+                    WT[k][4 * q] = v.x;
+                    WT[k][4 * q + 1] = v.y;
+                    WT[k][4 * q + 2] = v.z;
+                    WT[k][4 * q + 3] = v.w;
+                }
+            }
+            if (!__ballot(act[0] || act[1])) break;
+            uint32_t em[CH] = {0u, 0u};
+#pragma unroll
+            for (int j = 0; j < BLK; ++j) {
+                FlPend P[CH];
+#pragma unroll
+                for (int k = 0; k < CH; ++k)
+                    fl_issue<KR, NR>(base, F, GD, s_rows, act[k], w[k], (WT[k][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb[k],
+                                     H[k], P[k]);
+#pragma unroll
+                for (int k = 0; k < CH; ++k) fl_mid<KR, NR>(base, s_rows, act[k], H[k], P[k], own[k]);
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const uint32_t wn = fl_fin(P[k]);
+                    if (j > 0) {  // the output of position j - 1, which produced w
+                        const bool rec = (w[k] & DFA_STATE_MASK) >= F;
+                        const uint32_t code = w[k] >> 20;
+                        const bool esc = !rec && code == DFA_ESC;
+                        const uint32_t id = rec ? own[k] : code;
+                        if (kIds) {
+                            my[k][j - 1] = (uint16_t)(esc ? (w[k] & DFA_STATE_MASK) : id);
+                            em[k] |= esc ? 1u << (j - 1) : 0u;
+                        }
+                        cnt += act[k] && id != 0u;  // an escape is a nonzero id
+                    }
+                    w[k] = act[k] ? wn : w[k];
+                }
+            }
+            // position 31 of both chains
+#pragma unroll
+            for (int k = 0; k < CH; ++k) fl_out_issue<NR>(base, F, GD, w[k], cb[k], H[k]);
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                bool esc;
+                const uint32_t id = fl_out_get<NR>(F, GD, w[k], H[k], esc);
+                if (kIds) {
+                    my[k][BLK - 1] = (uint16_t)(esc ? (w[k] & DFA_STATE_MASK) : id);
+                    em[k] |= esc ? 1u << (BLK - 1) : 0u;
+                }
+                cnt += act[k] && id != 0u;
+            }
+            if (!kIds) continue;
+#pragma unroll
+            for (int k = 0; k < CH; ++k)
+                if (!act[k]) em[k] = 0;
+            while (__ballot(em[0] != 0 || em[1] != 0)) {  // row outputs past the inline code
+#pragma unroll
+                for (int k = 0; k < CH; ++k)
+                    if (em[k]) {
+                        const uint32_t j = __builtin_ctz(em[k]);
+                        em[k] &= em[k] - 1;
+                        my[k][j] = rowout16[my[k][j]];
+                    }
+            }
+            __builtin_amdgcn_wave_barrier();
+            // each chain set's block as dfa_fl_kernel stores it: whole lines
+            constexpr int LPC = OUTW == 4 ? 8 : 4, CPI = 64 / LPC, NST = 64 / CPI, BST = NST / 2;
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const uint64_t am = __ballot(act[k]);
+                uint32_t lds_off = ((uint32_t)(lane / LPC) * SROW + (OUTW == 4 ? 2u : 4u) * (lane % LPC)) * 4u;
+                uint32_t go = (uint32_t)(lane / LPC) * sl + (uint32_t)(16 / OUTW) * (lane % LPC);
+                asm volatile("" : "+v"(lds_off), "+v"(go));
+                const uint64_t mine = am >> (lane / LPC);
+                const bool full = am == ~0ull;
+                const uint8_t* const lb = reinterpret_cast<const uint8_t*>(wrows[k]) + lds_off;
+#pragma unroll
+                for (int t0 = 0; t0 < NST; t0 += BST) {
+                    tu32x4 vs[BST];
+#pragma unroll
+                    for (int t = t0; t < t0 + BST; ++t) {
+                        const uint32_t* src = reinterpret_cast<const uint32_t*>(lb + t * CPI * SROW * 4);
+                        if (OUTW == 4) {
+                            const uint32_t w0 = src[0], w1 = src[1];
+                            vs[t - t0] = tu32x4{w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
+                        } else {
+                            vs[t - t0] = tu32x4{src[0], src[1], src[2], src[3]};
+                        }
+                    }
+#pragma unroll
+                    for (int t = t0; t < t0 + BST; ++t) {
+                        const tu32x4 v = vs[t - t0];
+                        const int64_t step = (wseg + 64 * k + CPI * t) * seg_len + BLK * b;  // wave-uniform
+                        tu32x4* o = OUTW == 4
+                                        ? reinterpret_cast<tu32x4*>(reinterpret_cast<uint32_t*>(out) + step + go)
+                                        : reinterpret_cast<tu32x4*>(reinterpret_cast<uint16_t*>(out) + step + go);
+                        if (full || ((mine >> (CPI * t)) & 1u)) __builtin_nontemporal_store(v, o);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // the segments' last (< BLK) positions
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            for (int64_t i = lo[k] + BLK * ((hi[k] - lo[k]) / BLK); i < hi[k]; ++i) {
+                w[k] = fl_step<KR, NR>(base, F, GD, s_rows, w[k], text[i], cb[k], H[k], own[k]);
+                bool esc;
+                uint32_t id = fl_output(base, F, GD, w[k], cb[k], H[k], esc);
+                if (kIds && esc) id = rowout16[w[k] & DFA_STATE_MASK];
+                if (OUTW == 4) reinterpret_cast<uint32_t*>(out)[i - pos0] = id;
+                if (OUTW == 2) reinterpret_cast<uint16_t*>(out)[i - pos0] = (uint16_t)id;
+                cnt += id != 0u;
+            }
         }
     }
     if (count) {
@@ -2456,29 +2500,22 @@ constexpr int SDFA_LANES_PER_CU = 1024, SDFA_BLK = 32;
 // scripts/dfa_seg_sweep.py, profiles/r02/dfa_segment_sweep.txt).
 //
 // Product kernels of the sparse form (DfaDev::sparse_kernel 0; side by side
-// histories in DESIGN.md §4): the fallback-linked form (dfa_fl_kernel,
+// histories in MEASUREMENTS.md): the fallback-linked form (dfa_fl_kernel,
 // PM_SK_FL) at every width -- u32 / u16 ids staged in LDS, or the count
-// alone -- where the object has it (< 65,536 rows and gids); else for u32
-// ids the u16-staged 8-B-unit kernel (dfa_sparse_stage16_kernel<88, 4>,
-// PM_SK_STAGE16), with gids past u16 the u32-staged one (PM_SK_STAGE); for
-// u16 ids and the count the lock-step kernel over 8-B units (PM_SK_LOCK8);
-// without 8-B units (ids past 2^20) the lock-step kernel over the 16-B
-// records (PM_SK_LOCK16).
+// alone -- where the object has it (< 65,536 rows and gids); else the
+// lock-step kernel over 8-B units (PM_SK_LOCK8), and without 8-B units (ids
+// past 2^20) the lock-step kernel over the 16-B records (PM_SK_LOCK16).
 // A forced kernel (DfaDev::sparse_kernel; tests, A/B timing) runs where the
-// object has its image and it writes the width asked for; other launches
-// take the product choice (pm_dfa_sparse_choice reports which ran).
+// object has its image; other launches take the product choice
+// (pm_dfa_sparse_choice reports which ran, pm_hip_sparse_kernel_last).
 int pm_dfa_sparse_choice(const DfaDev& t, int outw) {
+    (void)outw;  // every sparse kernel writes every width
     if (!(t.coded && t.sbase && t.form != 1)) return 0;
     const int sk = t.sparse_kernel;
-    const bool ok = sk == PM_SK_FL       ? t.flbase != nullptr
-                    : sk == PM_SK_STAGE16 ? t.sout8h && outw == 4
-                    : sk == PM_SK_STAGE   ? t.sbase8 && outw != 0
-                    : sk == PM_SK_LOCK8   ? t.sbase8 != nullptr
-                                          : sk == PM_SK_LOCK16;
+    const bool ok = sk == PM_SK_FL ? t.flbase != nullptr : sk == PM_SK_LOCK8 ? t.sbase8 != nullptr : sk == PM_SK_LOCK16;
     if (ok) return sk;
     if (t.flbase) return PM_SK_FL;
-    return outw == 4 ? (t.sout8h ? PM_SK_STAGE16 : t.sbase8 ? PM_SK_STAGE : PM_SK_LOCK16)
-                     : (t.sbase8 ? PM_SK_LOCK8 : PM_SK_LOCK16);
+    return t.sbase8 ? PM_SK_LOCK8 : PM_SK_LOCK16;
 }
 
 hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
@@ -2491,7 +2528,8 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     const bool sparse = sk != 0;
     // segments: one per lane and chain, none shorter than short_seg, whole
     // blocks
-    const int64_t ch = !t.coded ? 1 : sparse ? 1 : DFA_CHAINS;
+    const bool fl2 = sk == PM_SK_FL && t.flchains == 2;  // dfa_fl2_kernel: two chains per lane
+    const int64_t ch = !t.coded ? 1 : sparse ? (fl2 ? 2 : 1) : DFA_CHAINS;
     const int lanes_cu = sparse ? SDFA_LANES_PER_CU : t.coded && outw == 0 ? DFA_COUNT_LANES_PER_CU : DFA_LANES_PER_CU;
     const int64_t lanes = (int64_t)num_cu * lanes_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
@@ -2503,8 +2541,8 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (sparse) {
         // persistent workgroups (LDS staged once each), at most one lane per
         // segment and SDFA_LANES_PER_CU lanes per CU
-        const int wgt = sk == PM_SK_FL || sk == PM_SK_STAGE16 || sk == PM_SK_STAGE ? 1024 : DFA_LDS_THREADS;
-        int64_t wg = (nseg + wgt - 1) / wgt;
+        const int wgt = sk == PM_SK_FL ? 1024 : DFA_LDS_THREADS;
+        int64_t wg = (nseg + wgt * ch - 1) / (wgt * ch);
         const int64_t cap = lanes / wgt;
         if (wg > cap) wg = cap;
         if (wg < 1) wg = 1;
@@ -2520,24 +2558,27 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
         else if (outw == 2) PM_FL_LAUNCH(FL_LDS_ROWS, 2, NR_);  \
         else PM_FL_LAUNCH(FL_COUNT_LDS_ROWS, 0, NR_);           \
     } while (0)
+                if (fl2) {  // two chains per lane (NR 1 or 2: the registers of two holds)
+#define PM_FL2_LAUNCH(KR_, W_, NR_)                                                                              \
+    hipLaunchKernelGGL((dfa_fl2_kernel<KR_, W_, NR_>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, \
+                       t.flbase, t.flF, t.flGD, t.flrowout16, t.warm, seg, g3)
+                    if (t.flhold == 1) {
+                        if (outw == 4) PM_FL2_LAUNCH(FL2_LDS_ROWS, 4, 1);
+                        else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 1);
+                        else PM_FL2_LAUNCH(FL_COUNT_LDS_ROWS, 0, 1);
+                    } else {
+                        if (outw == 4) PM_FL2_LAUNCH(FL2_LDS_ROWS, 4, 2);
+                        else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 2);
+                        else PM_FL2_LAUNCH(FL_COUNT_LDS_ROWS, 0, 2);
+                    }
+#undef PM_FL2_LAUNCH
+                    break;
+                }
                 if (t.flhold == 1) PM_FL_WIDTHS(1);  // every record as a 16-B half
                 else if (t.flhold == 4) PM_FL_WIDTHS(4);  // 64-B deep blocks
                 else PM_FL_WIDTHS(2);
 #undef PM_FL_WIDTHS
 #undef PM_FL_LAUNCH
-                break;
-            case PM_SK_STAGE16:
-                hipLaunchKernelGGL((dfa_sparse_stage16_kernel<88, 4, true>), gs, bs, 0, s, text, stream_start, pos0, n,
-                                   reinterpret_cast<uint32_t*>(out), count, t.sbase8, t.sF, t.sout8, t.sout8h, t.warm,
-                                   seg, g3);
-                break;
-            case PM_SK_STAGE:
-                if (outw == 4)
-                    hipLaunchKernelGGL((dfa_sparse_stage_kernel<4, 16, 1024, false, 4>), gs, bs, 0, s, text,
-                                       stream_start, pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
-                else
-                    hipLaunchKernelGGL((dfa_sparse_stage_kernel<2, 16, 1024, false, 4>), gs, bs, 0, s, text,
-                                       stream_start, pos0, n, out, count, t.sbase8, t.sF, t.sout8, t.warm, seg, g3);
                 break;
             case PM_SK_LOCK8:  // 8-B units, two blocks' text per load; LDS rows for ids only
                 if (outw == 4)

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <unistd.h>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -78,7 +79,13 @@ constexpr int AUTO_HOLD = 64;
 // measurement costs an RT launch and the DFA trials -- on the lines stream
 // ~3x and ~1-3.5x the held kernel's time -- so a fixed hold of 64 launches
 // spent ~20% of the time measuring.  reset() (a new stream) starts over.
+// Launches below AUTO_SMALL_LAUNCH positions (read_block's 100 KiB chunks,
+// measure.c:77) double only up to AUTO_STREAK_MAX_SMALL: 512 launches of
+// 100 KiB are 50 MiB before the next measurement instead of 400 MiB, so a
+// stream that turns from ASCII to deep lines is re-measured soon.
 constexpr int AUTO_STREAK_MAX = 6;
+constexpr int AUTO_STREAK_MAX_SMALL = 3;
+constexpr int64_t AUTO_SMALL_LAUNCH = 4ll << 20;
 // CAND_SPARSE16: the sparse form's fallback-linked kernel holding every
 // record as a 16-B half (DfaDev::flhold 1, FlImage::deep_g ignored): faster
 // where walks rarely stay in a record's block (snort, the tiled shipped
@@ -201,6 +208,9 @@ struct PmHip {
     bool cache_hit = false;
     std::vector<void*> allocs;
     size_t table_bytes = 0;
+    // start-up cost of the last compile() (pm_hip_compile_stats): wall
+    // seconds of the whole call and of its host-to-device table copies
+    double compile_s = 0.0, upload_s = 0.0;
     uint32_t* spill = nullptr;  // RT deep-walk scratch of captured scan_device launches (graphs)
     int64_t spill_cap = 0;
     std::vector<StreamSpill> sspill;  // ... and of direct ones, per stream (stream_spill)
@@ -270,7 +280,9 @@ void init_pick(AutoPick& a, int kind, bool has_sparse) {
 void* dalloc_copy(PmHip* o, const void* src, size_t bytes) {
     void* p = nullptr;
     PM_CHECK(hipMalloc(&p, bytes ? bytes : 16));
+    const auto t0 = std::chrono::steady_clock::now();
     if (bytes) PM_CHECK(hipMemcpy(p, src, bytes, hipMemcpyHostToDevice));
+    o->upload_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     o->allocs.push_back(p);
     o->table_bytes += bytes;
     return p;
@@ -426,14 +438,22 @@ unsigned host_threads() {
 // stays valid while it runs (the caller waits for every piece before
 // returning).  PM_HOST_POOL = the workers (default 3, at most the core share
 // minus one; 0 = no pool).  The pool is a static object: its destructor (at
-// exit or when the library is unloaded) wakes the workers and joins them.
+// exit or when the library is unloaded) wakes the workers and joins them --
+// in the process that started them only.  A child forked after the pool
+// started holds std::thread objects whose threads do not exist in it (and
+// maybe a mutex some worker held at the fork), so there the destructor
+// touches neither the lock nor the threads: it detaches them.
 class HostPool {
 public:
-    explicit HostPool(unsigned workers) {
+    explicit HostPool(unsigned workers) : owner_(getpid()) {
         spin_us_ = std::max(0, env_int("PM_HOST_POOL_SPIN_US", core_share() >= 8 ? 200 : 0));
         for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
     }
     ~HostPool() {
+        if (getpid() != owner_) {
+            for (std::thread& t : th_) t.detach();
+            return;
+        }
         {
             std::lock_guard<std::mutex> l(m_);
             stop_.store(true, std::memory_order_seq_cst);
@@ -505,6 +525,7 @@ private:
     std::mutex submit_, m_;
     std::condition_variable cv_;
     long spin_us_ = 200;
+    const pid_t owner_;  // the process that started the workers
     std::vector<std::thread> th_;
 };
 
@@ -579,9 +600,11 @@ void start_trials(const PmHip* o, AutoPick& ap) {
     ap.trial = 0;
 }
 
-// The hold after a measurement chose ap.chosen (AUTO_STREAK_MAX).
+// The hold after a measurement chose ap.chosen (AUTO_STREAK_MAX; for small
+// launches AUTO_STREAK_MAX_SMALL).
 int confirm_hold(AutoPick& ap) {
-    ap.streak = ap.chosen == ap.prev ? std::min(ap.streak + 1, AUTO_STREAK_MAX) : 0;
+    const int cap = ap.n_of[ap.chosen] < AUTO_SMALL_LAUNCH ? AUTO_STREAK_MAX_SMALL : AUTO_STREAK_MAX;
+    ap.streak = ap.chosen == ap.prev ? std::min(ap.streak + 1, cap) : 0;
     ap.prev = ap.chosen;
     return AUTO_HOLD << ap.streak;
 }
@@ -883,6 +906,8 @@ void pm_hip_add_pattern(void* obj, char* pat, size_t len, pm_pattern_id_t id) {
 
 void pm_hip_compile(void* obj) {
     PmHip* o = as(obj);
+    const auto tc0 = std::chrono::steady_clock::now();
+    o->upload_s = 0.0;
     PM_CHECK(hipSetDevice(o->device));
     o->gids = pm_assign_gids(o->pats);
     o->kind = o->kind_req;
@@ -943,10 +968,6 @@ void pm_hip_compile(void* obj) {
                 b8.resize(b8.size() + 16, 0u);  // the last aligned 64-B block
                 o->dfa.sbase8 = (const uint8_t*)dalloc_copy(o, b8.data(), b8.size() * 4);
                 o->dfa.sout8 = (const uint32_t*)dalloc_copy(o, o8.data(), o8.size() * 4);
-                if (o->gids.index_of_gid.size() <= 65536) {  // half the escape table's footprint in L2
-                    std::vector<uint16_t> h(o8.begin(), o8.end());
-                    o->dfa.sout8h = (const uint16_t*)dalloc_copy(o, h.data(), h.size() * 2);
-                }
             }
             FlImage fl;  // the fallback-linked form (pm_pack_sparse_fl)
             const std::vector<uint8_t> prof = pm_fl_profile(o->pats);  // the LDS rows' profile
@@ -987,6 +1008,7 @@ void pm_hip_compile(void* obj) {
     o->id_of_gid.assign(o->gids.index_of_gid.size(), PM_NULL_PATTERN_ID);
     for (size_t g = 1; g < o->gids.index_of_gid.size(); ++g) o->id_of_gid[g] = o->ids[o->gids.index_of_gid[g]];
     o->compiled = true;
+    o->compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tc0).count();
 }
 
 void pm_hip_host_profile(int on, double* out5) {
@@ -1205,6 +1227,14 @@ void pm_hip_set_image_cache(void* obj, const char* dir) { as(obj)->cache_dir = d
 
 int pm_hip_image_cache_hit(void* obj) { return as(obj)->cache_hit ? 1 : 0; }
 
+int pm_hip_compile_stats(void* obj, double* compile_ms, double* upload_ms) {
+    const PmHip* o = as(obj);
+    if (!o->compiled) return -1;
+    if (compile_ms) *compile_ms = o->compile_s * 1e3;
+    if (upload_ms) *upload_ms = o->upload_s * 1e3;
+    return 0;
+}
+
 uint32_t pm_hip_parent_gid(void* obj, uint32_t gid) {
     PmHip* o = as(obj);
     if (!o->compiled || gid >= o->parent.size()) return UINT32_MAX;
@@ -1262,6 +1292,11 @@ int pm_hip_set_option(void* obj, const char* name, int64_t value) {
     if (k == "fl_hold") {
         if (value != 0 && value != 1 && value != 2 && value != 4) return -1;
         o->dfa.flhold = value ? (int)value : 2;
+        return 0;
+    }
+    if (k == "fl_chains") {
+        if (value < 0 || value > 2) return -1;
+        o->dfa.flchains = value ? (int)value : 1;
         return 0;
     }
     if (k == "dfa_sync") {

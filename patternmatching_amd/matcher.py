@@ -137,6 +137,19 @@ class HipMatcher:
         if self._dict is not None:
             self._codes = self.gid_codes(self._dict.codes())
 
+    def compile_stats(self):
+        """Start-up cost of the last compile(): {"compile_ms", "upload_ms",
+        "image_bytes", "image_cache_hit"} (pm_hip_compile_stats)."""
+        c, u = ctypes.c_double(), ctypes.c_double()
+        if self.lib.pm_hip_compile_stats(self.obj, ctypes.byref(c), ctypes.byref(u)) != 0:
+            raise RuntimeError("compile_stats before compile()")
+        return {"compile_ms": round(c.value, 2), "upload_ms": round(u.value, 2),
+                "image_bytes": int(self.lib.pm_hip_table_bytes(self.obj)),
+                "image_cache_hit": bool(self.lib.pm_hip_image_cache_hit(self.obj))}
+
+    def set_image_cache(self, directory: str):
+        self.lib.pm_hip_set_image_cache(self.obj, directory.encode())
+
     def read_char(self, c: int):
         return self.lib.pm_hip_read_char(self.obj, bytes([c]))
 
@@ -277,7 +290,11 @@ class HipMatcher:
 
     @property
     def device_seconds(self):
-        return self.lib.pm_hip_device_seconds(self.obj)
+        """Device seconds of read_block's scans since reset(), or None when
+        some of them were untimed (small calls with the "host_events" option
+        off, its default: pm_hip_device_seconds returns -1)."""
+        v = self.lib.pm_hip_device_seconds(self.obj)
+        return None if v < 0 else v
 
     def __del__(self):
         try:

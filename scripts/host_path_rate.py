@@ -44,7 +44,10 @@ for kind in ("rt", "ac"):
                 lib.pm_hip_read_block(m.obj, part.ctypes.data_as(ctypes.c_char_p), len(part), ids)
         dt = time.perf_counter() - t0
         res[f"{kind}_read_block_{api}_GBps"] = round(n / dt / 1e9, 3)
-    res[f"{kind}_device_seconds"] = round(lib.pm_hip_device_seconds(m.obj), 4)
+    # -1 = unmeasured: small calls are untimed unless the "host_events"
+    # option is on (include/pm_hip.h), and timing them costs ~7 us a call
+    dev_s = lib.pm_hip_device_seconds(m.obj)
+    res[f"{kind}_device_seconds"] = round(dev_s, 4) if dev_s >= 0 else None
 
 # raw PCIe copy rates between pinned host memory and HBM (the host path moves
 # 1 B up and 4 B (gid) down per position)

@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """Side by side, one process: the sparse AC-DFA form's kernels (the
 per-object "sparse_kernel" option, include/pm_hip.h: 1 fallback-linked,
-2 u16-staged 8-B units, 3 u32-staged, 4 lock-step 8-B units, 5 lock-step
-16-B records) on 1 GiB of each stream, ids checked equal across kernels.
+2 lock-step 8-B units, 3 lock-step 16-B records) on 1 GiB of each stream, ids checked equal across kernels.
 With PM_LIBPM naming another build of the library (scripts/build_ab.sh, e.g.
 an ablation build with -DPM_FL_SPEC=2) the same for that build: run it once
 per build (scripts/ab_libs.sh alternates them).  Prints one JSON object."""

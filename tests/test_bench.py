@@ -78,6 +78,28 @@ def test_gpus_flag_starts_that_many_ranks_without_a_launcher():
     assert d["cpu_baseline"]["value"] > 0
 
 
+def test_eight_rank_rehearsal_shares_one_compile(tmp_path):
+    """The driver's 8-GPU run, rehearsed on the CPU: `bench.py --gpus 8`
+    starts eight ranks (gloo), and the start-up protocol runs for real on the
+    host -- rank 0 flattens the automaton into the image cache, ranks 1-7
+    read it after the barrier instead of compiling (measure.c:324-332's
+    loop is what the ranks then shard).  Every rank reports its start-up."""
+    cache = tmp_path / "imgcache"
+    r = _rehearse(["--gpus", "8", "--dict", "et", "--no-cpu", "--no-extra", "--image-cache", str(cache)])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["rehearsal"] and d["n_gpus"] == 8 and d["world_size"] == 8
+    assert d["rank_sum"] == 36.0 and sorted(x["rank"] for x in d["per_rank"]) == list(range(8))
+    assert len({x["pid"] for x in d["per_rank"]}) == 8
+    su = {x["rank"]: x["startup"] for x in d["per_rank"]}
+    assert su[0]["image_cache"] == "miss"
+    assert all(su[k]["image_cache"] == "hit" for k in range(1, 8)), su
+    assert all(su[k]["compile_ms"] > 0 and su[k]["dict_load_ms"] > 0 for k in range(8))
+    assert any(p.name.endswith(".img") for p in cache.iterdir())
+
+
 def test_world_size_mismatch_is_an_error():
     r = _rehearse(["--gpus", "4", "--no-cpu"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

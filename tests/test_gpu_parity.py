@@ -479,7 +479,7 @@ def test_small_calls_changing_sizes(kind):
             m.reset()
             parts = [m.read_block_gids(text[a:b]) for a, b in zip(offs[:-1], offs[1:])]
             assert np.array_equal(np.concatenate(parts), whole), ev
-            assert (m.device_seconds > 0) if ev else (m.device_seconds == -1.0)
+            assert (m.device_seconds > 0) if ev else (m.device_seconds is None and m.lib.pm_hip_device_seconds(m.obj) == -1.0)
             m.reset()
             ids = [m.read_block_id_array(text[a:b]) for a, b in zip(offs[:-1], offs[1:])]
             assert np.array_equal(np.concatenate(ids), whole_ids), ev
@@ -488,11 +488,11 @@ def test_small_calls_changing_sizes(kind):
         if kind == "rt":
             assert m.set_option("rt_small_max", 0) == 0  # the chunked RT kernel from here on
         else:
-            assert m.set_option("dfa_form", 2) == 0 and m.set_option("sparse_kernel", 4) == 0
+            assert m.set_option("dfa_form", 2) == 0 and m.set_option("sparse_kernel", 2) == 0
         parts += [m.read_block_gids(text[a:b]) for a, b in zip(offs[7:-1], offs[8:])]
         assert np.array_equal(np.concatenate(parts), whole)
         if kind == "ac":
-            assert m.sparse_kernel_last == 4
+            assert m.sparse_kernel_last == 2
     finally:
         for k, v in (("host_events", -1), ("rt_small_max", -1), ("dfa_form", 0), ("sparse_kernel", 0)):
             m.set_option(k, v)
@@ -890,8 +890,9 @@ def test_sparse_dfa_equals_dense_dfa(key, stream):
         ac.set_option("dfa_sync", 1)
 
 
-# the sparse form's kernels ("sparse_kernel" option) and the widths each writes
-SPARSE_KERNELS = {1: (4, 2, 0), 2: (4,), 3: (4, 2), 4: (4, 2, 0), 5: (4, 2, 0)}
+# the sparse form's kernels ("sparse_kernel": 1 fallback-linked, 2 lock-step
+# 8-B units, 3 lock-step 16-B records) and the widths each writes
+SPARSE_KERNELS = {1: (4, 2, 0), 2: (4, 2, 0), 3: (4, 2, 0)}
 
 
 @pytest.mark.parametrize("key", ["et", "merged"])
@@ -958,7 +959,7 @@ def test_sparse_form_without_8b_units():
     20 letters, 916,050 states -- larger than merged's) has the sparse form
     but neither the 8-B nor the fallback-linked layout (gids past u16): its
     u32 scans and its count take the lock-step kernel over the 16-B records
-    (sparse_kernel 5) and equal the dense rows' (no 8-B-unit
+    (sparse_kernel 3) and equal the dense rows' (no 8-B-unit
     kernel may run on the missing image)."""
     torch = _torch()
     rng = np.random.default_rng(7)
@@ -981,7 +982,7 @@ def test_sparse_form_without_8b_units():
             m.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c.data_ptr(), s)
             torch.cuda.synchronize()
             if form == 2:
-                assert m.sparse_kernel_last == 5
+                assert m.sparse_kernel_last == 3
             cc = torch.zeros(1, dtype=torch.int64, device="cuda")
             m.scan_device(dt.data_ptr(), 0, 0, n, 0, cc.data_ptr(), s)
             torch.cuda.synchronize()
@@ -996,9 +997,9 @@ def test_sparse_form_without_8b_units():
 
 @pytest.mark.parametrize("stream", ["lines", "ship"])
 def test_sparse_dfa_kernel_variants_agree(stream):
-    """Every product kernel of the sparse form ("sparse_kernel" 1-5: the
-    fallback-linked form, the u16- and u32-staged 8-B-unit kernels, the
-    lock-step kernels over 8-B units and 16-B records), under both warm-up
+    """Every kernel of the sparse form ("sparse_kernel" 1-3: the
+    fallback-linked form, the lock-step kernels over 8-B units and 16-B
+    records), under both warm-up
     rules, gives the RT kernel's u32 / u16 ids and the same count, at sizes
     from one warm-up segment to 32 MiB (snort); a width a kernel does not
     write runs the product choice, and pm_hip_sparse_kernel_last says which

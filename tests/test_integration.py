@@ -138,6 +138,46 @@ def test_reference_loop_per_byte_rate(tmp_path):
     assert rates["HIP Reverse-Trie"] >= rates["Aho-Corasick"], rates
 
 
+# /root/reference/results.csv:2-3, the reference's published run
+# `-d snort.dict -d et.dict -s dictionaries_generated.stream`:
+# AC 716,744 states x 2,072 B + 24 B; LMAC's list nodes.
+PUBLISHED_AC_MEMORY = 1485093592
+PUBLISHED_LMAC_MEMORY = 40137664
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slots", [("auto", "rt"), ("auto", None)], ids=["bg_auto+lmac_rt", "bg_auto+lmac_ref"])
+def test_reference_published_run_reproduced(tmp_path, slots):
+    """The reference's published command, literally, through its own program
+    with the batch call (oracle/_ref/ref_loop_batched): both dictionaries in
+    results.csv's order and the shipped stream.  The AC row's Total Memory
+    Used equals results.csv:2 (and, with the reference's LMAC kept in its
+    slot, LMAC's equals results.csv:3); every row, the HIP ones included, has
+    zero false-positive, false-negative and partial rates against the
+    reference AC (measure.c:300-303)."""
+    assert os.path.exists(REF_LOOP_BATCHED), "build it in the build container: make -C oracle refloopb"
+    bg, lmac = slots
+    res = _ref_loop(tmp_path, ["snort.dict", "et.dict"], os.path.join(DATA, "dictionaries_generated.stream"), bg,
+                    lmac, exe=REF_LOOP_BATCHED)
+    want = {"Aho-Corasick", "HIP Auto (RT / AC per launch)",
+            "HIP Reverse-Trie" if lmac else "Low-Memory Aho-Corasick"}
+    assert set(res) == want, res.keys()
+    assert int(res["Aho-Corasick"]["Total Memory Used"]) == PUBLISHED_AC_MEMORY
+    if not lmac:
+        assert int(res["Low-Memory Aho-Corasick"]["Total Memory Used"]) == PUBLISHED_LMAC_MEMORY
+    for name, row in res.items():
+        assert float(row["False Positive Rate"]) == 0.0, (name, row)
+        assert float(row["False Negative Rate"]) == 0.0, (name, row)
+        assert float(row["Partial Success Rate"]) == 0.0, (name, row)
+        assert int(row["Total Memory Used"]) > 0
+    ev = os.environ.get("PM_EVIDENCE_DIR")
+    if ev:
+        os.makedirs(ev, exist_ok=True)
+        tag = f"bg_{bg}_lmac_{lmac or 'ref'}"
+        with open(tmp_path / "results.csv") as src, open(os.path.join(ev, f"published_run_{tag}.csv"), "w") as dst:
+            dst.write(src.read())
+
+
 @pytest.mark.gpu
 def test_reference_loop_with_the_batch_call_is_exact(tmp_path):
     """The reference's program with INTEGRATION.md §2's batch call
