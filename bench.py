@@ -47,7 +47,7 @@ DICTS = {"et": ["et.dict"], "snort": ["snort.dict"], "merged": ["snort.dict", "e
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 WIDTH = {"dense": 4, "dense16": 2, "count": 0}  # bytes written per stream position
 CAND_NAME = {0: "RT", 1: "RT", 2: "AC dense rows", 3: "AC rows + records", 4: "AC rows + records (16-B record loads)",
-             5: "AC rows + records (64-B deep blocks)"}
+             5: "AC rows + records (64-B deep blocks)", 6: "AC rows + records (two chains per lane)"}
 # a reference AC object per CPU-baseline process: snort's table is ~1.06 GB
 # (2072 B per state, mpac.c:43-48), so the process count is also bounded by memory
 REF_PROC_BYTES = 1_300_000_000
@@ -66,7 +66,7 @@ def parse(argv=None):
                    help="rt: reverse-trie kernel; ac: the AC-DFA (dense rows or rows + records, timed); "
                         "auto: RT or the AC-DFA, picked per launch")
     p.add_argument("--stream", default="ascii", choices=["ascii", "bytes", "ship", "lines"],
-                   help="ascii / bytes: seeded synthetic (DESIGN.md §5); ship: the reference's shipped "
+                   help="ascii / bytes: seeded synthetic (DESIGN.md §6); ship: the reference's shipped "
                         "dictionaries_generated.stream tiled to --bytes (adversarial: deep matches); lines: "
                         "the dictionary's patterns drawn at random, '\\n' after each (deep, no period)")
     p.add_argument("--seed", type=int, default=1)
@@ -458,7 +458,7 @@ def main():
 
     def timed(matcher, steps, warmup, optr, w, cnt):
         """Pick phase (ac / auto: launches synchronized one by one until the
-        kind holds a choice, at most 12), W warmups, the hold pinned over the
+        kind holds a choice, at most 16), W warmups, the hold pinned over the
         timed steps, then `steps` launches between synchronizations and
         barriers.  Returns (elapsed s, mean kernel ms from hipEvents on the
         launch stream, held choice)."""
@@ -466,7 +466,7 @@ def main():
             matcher.scan_device(text.data_ptr(), 0, pos0, n, optr, cnt.data_ptr(), stream.cuda_stream,
                                 out_width=w or 4)
         held = matcher.hold_choice(0)
-        for _ in range(12):
+        for _ in range(16):
             if held != -1:
                 break
             step()
@@ -611,7 +611,7 @@ def main():
                 "stream_gbps": round(world * n / (d_ms * 1e-3) / 1e9, 2),
                 "matches_per_step": int(d_matches), "matches_per_sec": round(d_matches / (d_ms * 1e-3), 1),
                 "data": "synthetic deep-match stream: the dictionary's own patterns drawn at random (splitmix64 "
-                        "per 1 KiB block), '\\n' after each, generated in HBM (DESIGN.md §5)",
+                        "per 1 KiB block), '\\n' after each, generated in HBM (DESIGN.md §6)",
                 "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": n * 5,
                              "traffic": dtr["traffic_bytes"] if dtr else None,
@@ -647,8 +647,8 @@ def main():
             "data": {"ship": "the reference's shipped Streams/dictionaries_generated.stream (10,240 B) tiled in "
                              "HBM; dictionaries from the reference",
                      "lines": "synthetic deep-match stream: the dictionary's own patterns drawn at random "
-                              "(splitmix64 per 1 KiB block), '\\n' after each, generated in HBM (DESIGN.md §5)"}.get(
-                args.stream, "synthetic: seeded splitmix64 %s stream per GPU (DESIGN.md §5), generated in HBM; "
+                              "(splitmix64 per 1 KiB block), '\\n' after each, generated in HBM (DESIGN.md §6)"}.get(
+                args.stream, "synthetic: seeded splitmix64 %s stream per GPU (DESIGN.md §6), generated in HBM; "
                              "dictionaries from the reference" % args.stream),
             "config": {
                 "workload": f"{args.dict}.dict, {n} B {args.stream} stream per GPU, "
@@ -738,7 +738,7 @@ def other_configs(args, pm, lib, world, all_reduce, dist, text, out):
         def step():
             m.scan_device(t.data_ptr(), 0, 0, nbytes, o.data_ptr(), cnt.data_ptr(), stream.cuda_stream)
         held = m.hold_choice(0)
-        for _ in range(12):
+        for _ in range(16):
             if held != -1:
                 break
             step()

@@ -46,7 +46,7 @@ void* pm_hip_rt_create(void);
 void* pm_hip_ac_create(void);
 /* Both kernels; each launch picks one: the RT kernel, unless the last RT
  * launch spilled more than 10% of its positions (dense deep matches), when
- * the next 64 launches run the AC-DFA kernel (DESIGN.md §4).  reset()
+ * the next 64 launches run the AC-DFA kernel (DESIGN.md §5).  reset()
  * forgets the choice. */
 void* pm_hip_auto_create(void);
 void pm_hip_add_pattern(void* obj, char* pat, size_t len, pm_pattern_id_t id);
@@ -113,7 +113,8 @@ int pm_hip_pattern_counts_device(void* obj, const uint32_t* d_ids, int64_t n, un
  * (pm_hip_auto_create) for at least the next `launches` launches, so a timed
  * region never re-measures.  Returns the held kernel (1 = reverse trie,
  * 2 = AC dense rows, 3 = AC rows + records, 4 = the same with every record
- * loaded as a 16-B half, 5 = the same with deep records' 64-B blocks), 0
+ * loaded as a 16-B half, 5 = the same with deep records' 64-B blocks,
+ * 6 = the same with every record as a 16-B half and two segments per lane), 0
  * when the object has no choice
  * to make (rt kind, or a single DFA form), -1 while the pick is still being
  * measured (launch more, synchronize, and ask again). */
@@ -153,7 +154,7 @@ uint32_t pm_hip_parent_gid(void* obj, uint32_t gid);
 int pm_hip_gen_stream_device(uint8_t* d_dst, uint64_t offset, uint64_t n, uint64_t seed, int mode,
                              void* hip_stream);
 void pm_gen_stream_host(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode);
-/* The "lines" stream (DESIGN.md §5): 1 KiB blocks of the object's patterns
+/* The "lines" stream (DESIGN.md §6): 1 KiB blocks of the object's patterns
  * drawn at random (splitmix64), each followed by '\n' -- dense deep matches
  * without the period of a tiled file.  Device and host give the same bytes. */
 int pm_hip_gen_lines_device(void* obj, uint8_t* d_dst, uint64_t n, uint64_t seed, void* hip_stream);

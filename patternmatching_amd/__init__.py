@@ -10,7 +10,7 @@ interface:
     Dictionary      Core/src/PatternsTree.c:260-312 + parser.c:63-99
     HipMatcher      one MpsElem instance (create / add_pattern / compile /
                     read_char / read_block / reset / total_mem / free)
-    gen_stream      the synthetic stream specification (DESIGN.md §5)
+    gen_stream      the synthetic stream specification (DESIGN.md §6)
 """
 from ._lib import load, LIB_PATH, CLI_PATH  # noqa: F401
 from .matcher import (  # noqa: F401

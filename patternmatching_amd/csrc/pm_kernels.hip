@@ -2047,26 +2047,32 @@ __global__ __launch_bounds__(1024) void dfa_fl2_kernel(
     }
     for (int64_t wv = (int64_t)blockIdx.x * (THREADS / 64) + wid; wv * 64 * CH < nseg; wv += nwaves) {  // uniform
         const int64_t wseg = wv * 64 * CH;
-        int64_t lo[CH], hi[CH], wlo[CH];
+        // len: the chain's segment length (0: no segment); the warm-up is
+        // the wn bytes before the segment
+        uint32_t len[CH], wn[CH];
+        const uint8_t* wp[CH];
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
             const int64_t sg = wseg + 64 * k + lane;
             const bool has = sg < nseg;
-            lo[k] = has ? pos0 + sg * seg_len : pos0 + n;
-            hi[k] = has ? (lo[k] + seg_len < pos0 + n ? lo[k] + seg_len : pos0 + n) : pos0 + n;
-            wlo[k] = !has ? lo[k] : lo[k] - warm < stream_start ? stream_start : lo[k] - warm;
-            if (gram3) wlo[k] = dfa_sync_lo(text, lo[k], wlo[k], gram3);
+            const int64_t lo = has ? pos0 + sg * seg_len : pos0 + n;
+            const int64_t hi = has ? (lo + seg_len < pos0 + n ? lo + seg_len : pos0 + n) : pos0 + n;
+            int64_t wlo = !has ? lo : lo - warm < stream_start ? stream_start : lo - warm;
+            if (gram3) wlo = dfa_sync_lo(text, lo, wlo, gram3);
+            len[k] = (uint32_t)(hi - lo);
+            wn[k] = (uint32_t)(lo - wlo);
+            wp[k] = text + wlo;
             w[k] = 0;  // the root, reached by no word
         }
         // the warm-ups, both chains in lock step
-        for (int64_t t = 0; __ballot(wlo[0] + t < lo[0] || wlo[1] + t < lo[1]); ++t) {
+        for (uint32_t t = 0; __ballot(t < wn[0] || t < wn[1]); ++t) {
             bool on[CH];
             uint32_t cc[CH];
             FlPend P[CH];
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
-                on[k] = wlo[k] + t < lo[k];
-                cc[k] = on[k] ? text[wlo[k] + t] : 0u;
+                on[k] = t < wn[k];
+                cc[k] = on[k] ? wp[k][t] : 0u;
             }
 #pragma unroll
             for (int k = 0; k < CH; ++k) fl_issue<KR, NR>(base, F, GD, s_rows, on[k], w[k], cc[k], cb[k], H[k], P[k]);
@@ -2081,7 +2087,7 @@ __global__ __launch_bounds__(1024) void dfa_fl2_kernel(
             uint32_t WT[CH][8];
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
-                act[k] = lo[k] + BLK * b + BLK <= hi[k];
+                act[k] = (uint32_t)(BLK * b + BLK) <= len[k];
                 const uint8_t* const tb = text + pos0 + (wseg + 64 * k) * seg_len;  // wave-uniform
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
@@ -2096,31 +2102,43 @@ __global__ __launch_bounds__(1024) void dfa_fl2_kernel(
             }
             if (!__ballot(act[0] || act[1])) break;
             uint32_t em[CH] = {0u, 0u};
+            // four positions per iteration, not unrolled further: the
+            // dword of each chain's text in use is WT[k][0], shifted down
+            // after each iteration (a fully unrolled block kept too much
+            // live and spilled)
+#pragma unroll 1
+            for (uint32_t q = 0; q < BLK / 4; ++q) {
 #pragma unroll
-            for (int j = 0; j < BLK; ++j) {
-                FlPend P[CH];
+                for (int jj = 0; jj < 4; ++jj) {
+                    const uint32_t j = 4 * q + jj;
+                    FlPend P[CH];
+#pragma unroll
+                    for (int k = 0; k < CH; ++k)
+                        fl_issue<KR, NR>(base, F, GD, s_rows, act[k], w[k], (WT[k][0] >> (8 * jj)) & 0xFFu, cb[k], H[k],
+                                         P[k]);
+#pragma unroll
+                    for (int k = 0; k < CH; ++k) fl_mid<KR, NR>(base, s_rows, act[k], H[k], P[k], own[k]);
+#pragma unroll
+                    for (int k = 0; k < CH; ++k) {
+                        const uint32_t wn = fl_fin(P[k]);
+                        if (jj > 0 || q > 0) {  // the output of position j - 1, which produced w
+                            const bool rec = (w[k] & DFA_STATE_MASK) >= F;
+                            const uint32_t code = w[k] >> 20;
+                            const bool esc = !rec && code == DFA_ESC;
+                            const uint32_t id = rec ? own[k] : code;
+                            if (kIds) {
+                                my[k][j - 1] = (uint16_t)(esc ? (w[k] & DFA_STATE_MASK) : id);
+                                em[k] |= esc ? 1u << (j - 1) : 0u;
+                            }
+                            cnt += act[k] && id != 0u;  // an escape is a nonzero id
+                        }
+                        w[k] = act[k] ? wn : w[k];
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < CH; ++k)
-                    fl_issue<KR, NR>(base, F, GD, s_rows, act[k], w[k], (WT[k][j >> 2] >> (8 * (j & 3))) & 0xFFu, cb[k],
-                                     H[k], P[k]);
 #pragma unroll
-                for (int k = 0; k < CH; ++k) fl_mid<KR, NR>(base, s_rows, act[k], H[k], P[k], own[k]);
-#pragma unroll
-                for (int k = 0; k < CH; ++k) {
-                    const uint32_t wn = fl_fin(P[k]);
-                    if (j > 0) {  // the output of position j - 1, which produced w
-                        const bool rec = (w[k] & DFA_STATE_MASK) >= F;
-                        const uint32_t code = w[k] >> 20;
-                        const bool esc = !rec && code == DFA_ESC;
-                        const uint32_t id = rec ? own[k] : code;
-                        if (kIds) {
-                            my[k][j - 1] = (uint16_t)(esc ? (w[k] & DFA_STATE_MASK) : id);
-                            em[k] |= esc ? 1u << (j - 1) : 0u;
-                        }
-                        cnt += act[k] && id != 0u;  // an escape is a nonzero id
-                    }
-                    w[k] = act[k] ? wn : w[k];
-                }
+                    for (int i = 0; i < 7; ++i) WT[k][i] = WT[k][i + 1];
             }
             // position 31 of both chains
 #pragma unroll
@@ -2150,7 +2168,7 @@ __global__ __launch_bounds__(1024) void dfa_fl2_kernel(
             }
             __builtin_amdgcn_wave_barrier();
             // each chain set's block as dfa_fl_kernel stores it: whole lines
-            constexpr int LPC = OUTW == 4 ? 8 : 4, CPI = 64 / LPC, NST = 64 / CPI, BST = NST / 2;
+            constexpr int LPC = OUTW == 4 ? 8 : 4, CPI = 64 / LPC, NST = 64 / CPI, BST = 2;
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
                 const uint64_t am = __ballot(act[k]);
@@ -2189,7 +2207,8 @@ __global__ __launch_bounds__(1024) void dfa_fl2_kernel(
         // the segments' last (< BLK) positions
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
-            for (int64_t i = lo[k] + BLK * ((hi[k] - lo[k]) / BLK); i < hi[k]; ++i) {
+            const int64_t lo = pos0 + (wseg + 64 * k + lane) * seg_len;
+            for (int64_t i = lo + BLK * (len[k] / BLK); i < lo + len[k]; ++i) {
                 w[k] = fl_step<KR, NR>(base, F, GD, s_rows, w[k], text[i], cb[k], H[k], own[k]);
                 bool esc;
                 uint32_t id = fl_output(base, F, GD, w[k], cb[k], H[k], esc);
@@ -2489,7 +2508,7 @@ hipError_t pm_launch_rt_floor(const uint8_t* text, int64_t n, void* out, int out
 constexpr int DFA_LANES_PER_CU = 512, DFA_COUNT_LANES_PER_CU = 1024, DFA_CHAINS = 2, DFA_DENSE_BLK = 32;
 // The sparse form: 1,024 lanes per CU (two 512-lane lock-step workgroups,
 // or one 1,024-lane staged workgroup), one chain per lane, 32-position
-// blocks (profiles/r03/sdfa_lanes_*.txt, sdfa_occupancy_sweep.txt:
+// blocks (MEASUREMENTS.md §4, profiles/r03/sdfa_lanes_*.txt, sdfa_occupancy_sweep.txt:
 // past 1,024 lanes per CU every stream slows down).
 constexpr int SDFA_LANES_PER_CU = 1024, SDFA_BLK = 32;
 // Shortest segment: a launch of fewer segments than lanes is latency-bound

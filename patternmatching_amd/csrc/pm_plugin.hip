@@ -58,7 +58,7 @@ enum Kind { KIND_RT = 1, KIND_AC = 2, KIND_AUTO = 3 };
 
 // KIND_AUTO holds both images and picks a kernel per launch: the RT kernel
 // reports how many candidates it spilled (its queue overflowed: dense deep
-// matches -- DESIGN.md §4; a count-only launch, which queues nothing,
+// matches -- DESIGN.md §5; a count-only launch, which queues nothing,
 // reports the positions its tail walked) and its time; when a launch
 // reported more than AUTO_SPILL_FRAC of its positions, the next launches
 // try the AC-DFA kernel in each of its forms (dense rows, then rows +
@@ -95,7 +95,20 @@ constexpr int64_t AUTO_SMALL_LAUNCH = 4ll << 20;
 // lines 4.99 -> 4.87, merged lines 5.43 -> 5.13), slower elsewhere (shipped
 // 3.64, ASCII 3.07).  profiles/r05/ab/fl_hold_1_2_4.jsonl; all three timed
 // beside the other forms.
-enum Cand { CAND_RT = 0, CAND_DENSE = 1, CAND_SPARSE = 2, CAND_SPARSE16 = 3, CAND_SPARSE64 = 4, NCAND = 5 };
+// CAND_FL2: the same form, two chains per lane (dfa_fl2_kernel, records as
+// 16-B halves): faster where the walks' table lines stay in L2 (snort, the
+// tiled shipped stream 3.23 -> 2.54 ms, count 2.64 -> 1.96), slower where
+// they come from further out (lines 4.87 -> 6.31; ASCII 2.78 -> 3.30);
+// profiles/r06/fl2/.
+enum Cand {
+    CAND_RT = 0,
+    CAND_DENSE = 1,
+    CAND_SPARSE = 2,
+    CAND_SPARSE16 = 3,
+    CAND_SPARSE64 = 4,
+    CAND_FL2 = 5,
+    NCAND = 6
+};
 
 struct AutoPick {
     unsigned long long* d_spill = nullptr;  // device counter of the last measured RT launch
@@ -104,7 +117,7 @@ struct AutoPick {
     hipEvent_t t0[NCAND] = {}, t1[NCAND] = {};  // timing of each candidate's measured launch
     bool pending = false;     // a measured RT launch (spill count + time) in flight
     bool timing = false;      // the DFA trials are launched, their times in flight
-    int queue[4] = {0, 0, 0, 0};  // DFA forms to try, in order
+    int queue[NCAND] = {};    // DFA forms to try, in order
     int nq = 0, qi = 0;       // forms queued / started
     int trial = 0;            // launches left of the form being tried (the last one timed)
     int64_t n_of[NCAND] = {};
@@ -118,7 +131,7 @@ struct AutoPick {
 };
 
 // read_block pipeline blocks (positions): the upload, kernel and download of
-// block k overlap the host finishing block k-1 (DESIGN.md §5).  Gid output
+// block k overlap the host finishing block k-1 (DESIGN.md §2).  Gid output
 // is downloaded straight into the caller's array (no host work per block);
 // pattern-id output is mapped on the host, so smaller blocks overlap more
 // of that mapping with the transfers.
@@ -579,6 +592,10 @@ hipError_t launch_cand(PmHip* o, AutoPick& ap, int c, const uint8_t* text, int64
     d.form = c == CAND_DENSE ? 1 : 2;
     if (c == CAND_SPARSE16) d.flhold = 1;
     if (c == CAND_SPARSE64) d.flhold = 4;
+    if (c == CAND_FL2) {
+        d.flhold = 1;
+        d.flchains = 2;
+    }
     o->last_sparse_kernel = pm_dfa_sparse_choice(d, out ? outw : 0);
     return pm_launch_dfa(text, stream_start, pos0, n, out, outw, count, d, o->num_cu, s);
 }
@@ -594,6 +611,7 @@ void start_trials(const PmHip* o, AutoPick& ap) {
                     (o->dfa.sparse_kernel == PM_SK_PRODUCT || o->dfa.sparse_kernel == PM_SK_FL);
     if (o->dfa_form != 2 || !o->dfa.sbase) ap.queue[ap.nq++] = CAND_DENSE;
     if (fl) ap.queue[ap.nq++] = CAND_SPARSE16;
+    if (fl) ap.queue[ap.nq++] = CAND_FL2;
     if (o->dfa.sbase && o->dfa_form != 1) ap.queue[ap.nq++] = CAND_SPARSE;
     if (fl) ap.queue[ap.nq++] = CAND_SPARSE64;
     ap.qi = 0;
@@ -730,7 +748,7 @@ hipError_t launch(PmHip* o, const uint8_t* text, int64_t stream_start, int64_t p
 // For pattern ids, dictionaries of < 65,536 patterns (every reference
 // dictionary) come back as u16 gids (half the PCIe bytes) for the host
 // threads to map: +12% (RT) / +28% (AC).  Gids for the caller stay u32 and
-// direct: widening u16 on the host measured 2-5% slower.  Rates: DESIGN.md §5.
+// direct: widening u16 on the host measured 2-5% slower.  Rates: MEASUREMENTS.md §5.
 // Host-path breakdown (pm_hip_host_profile): seconds spent staging
 // the input, enqueueing the copies and the launch, waiting for the slot,
 // and copying / mapping the results; calls.

@@ -1,5 +1,5 @@
 // pm_streamgen.h -- synthetic stream generator (host and device), the
-// product's implementation of the stream specification in DESIGN.md §5:
+// product's implementation of the stream specification in DESIGN.md §6:
 //   word(k) = splitmix64((seed << 40) | k),  k = i / 8
 //   raw(i)  = (word(i/8) >> (8 * (i % 8))) & 0xFF
 //   mode 0 "ascii": 0x20 + ((raw * 95) >> 8)   mode 1 "bytes": raw

@@ -104,7 +104,7 @@ class Dictionary:
 
 
 def gen_stream(n, seed, mode=0, offset=0):
-    """Synthetic stream (DESIGN.md §5), host implementation."""
+    """Synthetic stream (DESIGN.md §6), host implementation."""
     lib = load()
     buf = np.empty(n, dtype=np.uint8)
     lib.pm_gen_stream_host(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), offset, n, seed, mode)

@@ -1,4 +1,4 @@
-// Scattered-load rate probe (what bounds the DFA kernel and
+// Scattered-load rate probe (MEASUREMENTS.md §4: what bounds the DFA kernel and
 // the RT tail).  Every lane runs `chains` independent pointer chases through
 // a table of random u32 indices (each load's address depends on the previous
 // load of its chain), `steps` loads per chain; prints loads/s for each

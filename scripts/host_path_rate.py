@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """PCIe-inclusive rate of the host-buffer boundary (read_block from host
-memory): times pm_hip_read_block_gid / pm_hip_read_block over a
+memory, MEASUREMENTS.md §5): times pm_hip_read_block_gid / pm_hip_read_block over a
 host stream in fixed-size calls, and the drop-in CLI end to end on a stream
 file.  Prints one JSON object."""
 import ctypes

@@ -1,6 +1,6 @@
 // sdfa_l2_model.cpp -- probe (not product): an LRU model of one XCD's 4 MiB L2 over
 // 16,384 interleaved lanes scanning the lines stream through the sparse AC-DFA,
-// for default-transition records of up to K = 2 / 12 / 28 slots.
+// for default-transition records of up to K = 2 / 12 / 28 slots (MEASUREMENTS.md §4).
 //   g++ -O2 -std=c++17 -Ipatternmatching_amd/csrc -Iinclude scripts/sdfa_l2_model.cpp \
 //       patternmatching_amd/csrc/pm_flatten.cpp patternmatching_amd/csrc/host/pm_dict.c -o /tmp/l2 && /tmp/l2 DICT...
 #include "pm_flatten.h"

@@ -699,14 +699,14 @@ def test_full_size_merged_deep_auto_oracle_windows(stream):
     a = torch.empty(n, dtype=torch.int32, device="cuda")
     c = torch.zeros(1, dtype=torch.int64, device="cuda")
     held = au.hold_choice(0)
-    for _ in range(12):  # the pick: launches synchronized one by one until it holds
+    for _ in range(16):  # the pick: launches synchronized one by one until it holds
         if held != -1:
             break
         au.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), None, s)
         torch.cuda.synchronize()
         held = au.hold_choice(0)
     held = au.hold_choice(2)
-    assert held in (1, 2, 3, 4, 5)
+    assert held in (1, 2, 3, 4, 5, 6)
     a.zero_()
     au.scan_device(dt.data_ptr(), 0, 0, n, a.data_ptr(), c.data_ptr(), s)
     torch.cuda.synchronize()
@@ -900,8 +900,9 @@ def test_fl_kernel_every_width(key):
     """The fallback-linked kernel (sparse_kernel 1) on et and the merged
     dictionaries, 8 MiB of each one's lines stream plus the shipped stream,
     with each record-load policy ("fl_hold": 16-B halves, deep records'
-    32-B and 64-B blocks): u32 ids, u16 ids and the count equal the
-    reverse-trie kernel's."""
+    32-B and 64-B blocks) and with two chains per lane ("fl_chains" 2,
+    dfa_fl2_kernel, 16-B halves and 32-B blocks): u32 ids, u16 ids and the
+    count equal the reverse-trie kernel's."""
     torch = _torch()
     rt, ac = matcher(key, "rt"), matcher(key, "ac")
     n = 8 << 20
@@ -909,7 +910,7 @@ def test_fl_kernel_every_width(key):
     dt = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     try:
         assert ac.set_option("dfa_form", 2) == 0 and ac.set_option("sparse_kernel", 1) == 0
-        assert ac.set_option("fl_hold", 3) == -1
+        assert ac.set_option("fl_hold", 3) == -1 and ac.set_option("fl_chains", 3) == -1
         for stream in ("lines", "ship"):
             if stream == "lines":
                 rt.gen_lines_device(dt.data_ptr(), n + 64, 21, s)
@@ -918,8 +919,8 @@ def test_fl_kernel_every_width(key):
             ref = torch.empty(n, dtype=torch.int32, device="cuda")
             rt.scan_device(dt.data_ptr(), 0, 0, n, ref.data_ptr(), None, s)
             nz = int((ref != 0).sum().item())
-            for hold in (1, 2, 4):
-                assert ac.set_option("fl_hold", hold) == 0
+            for hold, chains in ((1, 1), (2, 1), (4, 1), (1, 2), (2, 2)):
+                assert ac.set_option("fl_hold", hold) == 0 and ac.set_option("fl_chains", chains) == 0
                 a = torch.zeros(n, dtype=torch.int32, device="cuda")
                 h = torch.zeros(n, dtype=torch.int16, device="cuda")
                 c = torch.zeros(2, dtype=torch.int64, device="cuda")
@@ -930,11 +931,12 @@ def test_fl_kernel_every_width(key):
                 ac.scan_device(dt.data_ptr(), 0, 0, n, 0, c[1:2].data_ptr(), s)
                 assert ac.sparse_kernel_last == 1
                 torch.cuda.synchronize()
-                assert torch.equal(a, ref), (stream, hold)
-                assert torch.equal(h.to(torch.int32) & 0xFFFF, ref), (stream, hold)
-                assert int(c[0].item()) == nz and int(c[1].item()) == nz, (stream, hold)
+                assert torch.equal(a, ref), (stream, hold, chains)
+                assert torch.equal(h.to(torch.int32) & 0xFFFF, ref), (stream, hold, chains)
+                assert int(c[0].item()) == nz and int(c[1].item()) == nz, (stream, hold, chains)
     finally:
         ac.set_option("fl_hold", 0)
+        ac.set_option("fl_chains", 0)
         ac.set_option("sparse_kernel", 0)
         ac.set_option("dfa_form", 0)
 
@@ -1019,12 +1021,13 @@ def test_sparse_dfa_kernel_variants_agree(stream):
     try:
         # (2,567: 41 segments of 64, a wave with chains past 32 active, not all)
         for size, start in ((n, 0), (777, 4096), (2567, 8208), (100 << 10, 12345 & ~15), (5 << 20, 3 << 20)):
-            for sk, sync in [(k, y) for k in SPARSE_KERNELS for y in (0, 1)]:
+            for sk, sync, chains in [(k, y, 1) for k in SPARSE_KERNELS for y in (0, 1)] + [(1, 0, 2), (1, 1, 2)]:
                 assert ac.set_option("sparse_kernel", sk) == 0 and ac.set_option("dfa_sync", sync) == 0
+                assert ac.set_option("fl_chains", chains) == 0
                 a = torch.zeros(size, dtype=torch.int32, device="cuda")
                 h = torch.zeros(size, dtype=torch.int16, device="cuda")
                 c = torch.zeros(2, dtype=torch.int64, device="cuda")
-                tag = (size, sk, sync)
+                tag = (size, sk, sync, chains)
                 ac.scan_device(dt.data_ptr(), 0, start, size, a.data_ptr(), c[0:1].data_ptr(), s)
                 assert ac.sparse_kernel_last == sk, tag
                 ac.scan_device(dt.data_ptr(), 0, start, size, h.data_ptr(), None, s, out_width=2)
@@ -1037,6 +1040,7 @@ def test_sparse_dfa_kernel_variants_agree(stream):
                 assert int(c[0].item()) == int(c[1].item()) == int((a != 0).sum().item()), tag
     finally:
         ac.set_option("sparse_kernel", 0)
+        ac.set_option("fl_chains", 0)
         ac.set_option("dfa_sync", 1)
         ac.set_option("dfa_form", 0)
 
@@ -1068,11 +1072,13 @@ def test_dfa_warmups_stop_at_stream_start(stream):
             buf[stream_start:] = dt[: n + 64 - stream_start]
             ref = torch.empty(size, dtype=torch.int32, device="cuda")
             rt.scan_device(buf.data_ptr(), stream_start, pos0, size, ref.data_ptr(), None, s)
-            forms = [(1, 0, y) for y in (0, 1)] + [(2, k, y) for k in [0] + list(SPARSE_KERNELS) for y in (0, 1)]
-            for form, sk, sync in forms:
+            forms = [(1, 0, y, 1) for y in (0, 1)] + [(2, k, y, 1) for k in [0] + list(SPARSE_KERNELS) for y in (0, 1)]
+            forms += [(2, 1, y, 2) for y in (0, 1)]  # two chains per lane
+            for form, sk, sync, chains in forms:
                 ac.set_option("dfa_form", form)
                 ac.set_option("sparse_kernel", sk)
                 ac.set_option("dfa_sync", sync)
+                ac.set_option("fl_chains", chains)
                 a = torch.zeros(size, dtype=torch.int32, device="cuda")
                 h = torch.zeros(size, dtype=torch.int16, device="cuda")
                 c = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -1080,12 +1086,13 @@ def test_dfa_warmups_stop_at_stream_start(stream):
                 ac.scan_device(buf.data_ptr(), stream_start, pos0, size, h.data_ptr(), None, s, out_width=2)
                 ac.scan_device(buf.data_ptr(), stream_start, pos0, size, 0, c.data_ptr(), s)
                 torch.cuda.synchronize()
-                tag = (stream_start, pos0, form, sk, sync)
+                tag = (stream_start, pos0, form, sk, sync, chains)
                 assert torch.equal(a, ref), tag
                 assert torch.equal(h.to(torch.int32) & 0xFFFF, a), tag
                 assert int(c.item()) == int((a != 0).sum().item()), tag
     finally:
         ac.set_option("sparse_kernel", 0)
+        ac.set_option("fl_chains", 0)
         ac.set_option("dfa_sync", 1)
         ac.set_option("dfa_form", 0)
 
@@ -1177,7 +1184,7 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
     ref.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
     m = matcher("et", "auto")
     kernels, forms = [], []
-    for _ in range(12):
+    for _ in range(15):
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         m.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
@@ -1185,11 +1192,12 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
         forms.append(m.dfa_form_last)
         assert torch.equal(got, want)
     # RT first (measured: it spills), then two trial launches of each DFA
-    # candidate (dense rows; rows + records with 16-B, 32-B and 64-B record
-    # loads; the second of each timed); the fastest per position holds
-    assert kernels[:9] == [pm.KIND_RT] + [pm.KIND_AC] * 8, kernels
-    assert forms[:9] == [0, 1, 1, 2, 2, 2, 2, 2, 2], forms
-    assert len(set(zip(kernels[9:], forms[9:]))) == 1, (kernels, forms)
+    # candidate (dense rows; rows + records with 16-B halves, two chains per
+    # lane, 32-B and 64-B record loads; the second of each timed); the
+    # fastest per position holds
+    assert kernels[:11] == [pm.KIND_RT] + [pm.KIND_AC] * 10, kernels
+    assert forms[:11] == [0, 1, 1] + [2] * 8, forms
+    assert len(set(zip(kernels[11:], forms[11:]))) == 1, (kernels, forms)
 
 
 @pytest.mark.parametrize("cap", [1, 2])
@@ -1276,7 +1284,7 @@ def test_auto_scan_device_across_two_streams_and_hold():
     for o in outs:
         assert torch.equal(o, want)
     held = m.hold_choice(0)
-    for _ in range(12):
+    for _ in range(16):
         if held > 0:
             break
         o = outs[0]
@@ -1284,7 +1292,7 @@ def test_auto_scan_device_across_two_streams_and_hold():
         torch.cuda.synchronize()
         assert torch.equal(o, want)
         held = m.hold_choice(0)
-    assert held in (1, 2, 3, 4, 5), held
+    assert held in (1, 2, 3, 4, 5, 6), held
     assert m.hold_choice(100) == held  # pinned for the next 100 launches
     for _ in range(3):
         m.scan_device(dt.data_ptr(), 0, 0, n, outs[1].data_ptr(), None, streams[1].cuda_stream)
