@@ -2406,9 +2406,20 @@ static int64_t rt_blocks(int64_t n, int num_cu) {
 // equal (shipped 11.33-11.37 ms, lines 15.68-15.86 ms; random ASCII equal).
 // RtDev::spill_cap_chunks lowers it per object (tests: small launches then
 // resolve full regions many times).
+// The scratch is sized for RT_SPILL_CAP_CHUNKS, but a launch resolves its
+// region at a smaller default fill (round 6, scripts/rt_spillcap_ab.py,
+// profiles/r06/spillcap/): a region that fills is resolved inside the
+// chunk loop, where the other waves' streaming hides its probes, instead of
+// once after it, when every wave of the CU waits at the same time.  Count
+// only at 4 chunks: random ASCII 0.434 -> 0.411 ms (the shipped stream
+// equal, the lines stream +2.5%, which the auto kind gives to the DFA);
+// ids at 2 chunks: the shipped stream 11.39 -> 10.07 ms, the lines stream
+// 15.93 -> 13.90, random ASCII equal.
 constexpr int64_t RT_SPILL_CAP_CHUNKS = 16;
-static int64_t rt_wave_cap(int64_t cap_chunks) {
-    return (cap_chunks >= 1 && cap_chunks < RT_SPILL_CAP_CHUNKS ? cap_chunks : RT_SPILL_CAP_CHUNKS) * RT_CHUNK;
+constexpr int64_t RT_SPILL_FILL_COUNT = 4, RT_SPILL_FILL_IDS = 2;
+static int64_t rt_wave_cap(int64_t cap_chunks, int outw = -1) {
+    const int64_t dflt = outw < 0 ? RT_SPILL_CAP_CHUNKS : outw == 0 ? RT_SPILL_FILL_COUNT : RT_SPILL_FILL_IDS;
+    return (cap_chunks >= 1 && cap_chunks < RT_SPILL_CAP_CHUNKS ? cap_chunks : dflt) * RT_CHUNK;
 }
 static int64_t rt_spill_stride(int64_t n, int64_t blocks, int64_t wave_cap) {
     const int64_t nw = blocks * RT_WAVES;
@@ -2457,7 +2468,7 @@ static hipError_t launch_rt_impl(bool floor, const uint8_t* text, int64_t stream
     }
     const int64_t blocks = rt_blocks(n, num_cu);
     RtDev t = t0;
-    t.spill_stride = rt_spill_stride(n, blocks, rt_wave_cap(t0.spill_cap_chunks));
+    t.spill_stride = rt_spill_stride(n, blocks, rt_wave_cap(t0.spill_cap_chunks, out ? outw : 0));
     // The caller sizes the scratch (pm_rt_spill_items); a launch whose
     // scratch holds less than the stride clamps it to whole chunks, at least
     // one (the kernel resolves a full region and goes on, so any stride of

@@ -612,7 +612,11 @@ void start_trials(const PmHip* o, AutoPick& ap) {
     if (o->dfa_form != 2 || !o->dfa.sbase) ap.queue[ap.nq++] = CAND_DENSE;
     if (fl) ap.queue[ap.nq++] = CAND_SPARSE16;
     if (fl) ap.queue[ap.nq++] = CAND_FL2;
-    if (o->dfa.sbase && o->dfa_form != 1) ap.queue[ap.nq++] = CAND_SPARSE;
+    // (with the FL form the 32-B-block policy is not a candidate: it was the
+    // best on no stream measured -- snort / merged lines, the shipped stream,
+    // ASCII; profiles/r05/ab/fl_hold_1_2_4.jsonl -- and each candidate costs
+    // two launches per measurement)
+    if (o->dfa.sbase && o->dfa_form != 1 && !fl) ap.queue[ap.nq++] = CAND_SPARSE;
     if (fl) ap.queue[ap.nq++] = CAND_SPARSE64;
     ap.qi = 0;
     ap.trial = 0;

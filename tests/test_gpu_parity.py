@@ -1411,8 +1411,9 @@ def test_spill_cap_raised_after_prepare():
 @pytest.mark.parametrize("stream", ["ship", "lines"])
 def test_ac_kind_times_both_dfa_forms(stream):
     """The AC kind tries its forms (dense rows, rows + records, the latter
-    also with every record loaded as a 16-B half; two launches each, the
-    second timed) and holds the fastest; every launch equals the RT kernel."""
+    with each record-load policy and with two chains per lane; two launches
+    each, the second timed) and holds the fastest; every launch equals the
+    RT kernel."""
     import torch
     n = 16 << 20
     s = torch.cuda.current_stream()
@@ -1425,16 +1426,17 @@ def test_ac_kind_times_both_dfa_forms(stream):
     want = torch.empty(n, dtype=torch.int32, device="cuda")
     rt.scan_device(dt.data_ptr(), 0, 0, n, want.data_ptr(), None, s.cuda_stream)
     forms = []
-    for _ in range(11):
+    for _ in range(13):
         got = torch.empty(n, dtype=torch.int32, device="cuda")
         ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
         torch.cuda.synchronize()
         assert ac.kernel_last == pm.KIND_AC
         forms.append(ac.dfa_form_last)
         assert torch.equal(got, want)
-    # dense rows, then rows + records with 16-B, 32-B and 64-B record
-    # loads: two launches each, then the fastest holds
-    assert forms[:8] == [1, 1, 2, 2, 2, 2, 2, 2] and forms[8] == forms[9] == forms[10] in (1, 2), forms
+    # dense rows, then rows + records with 16-B halves, the same with two
+    # chains per lane, 32-B and 64-B record loads: two launches each, then
+    # the fastest holds
+    assert forms[:10] == [1, 1] + [2] * 8 and forms[10] == forms[11] == forms[12] in (1, 2), forms
     ac.reset()  # a new stream: the forms are timed again
     ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
     torch.cuda.synchronize()
