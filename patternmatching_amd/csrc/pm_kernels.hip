@@ -1624,6 +1624,13 @@ __device__ __forceinline__ int64_t wave_uniform64(int64_t v) {
 #define PM_FL_SPEC 0
 #endif
 static_assert(PM_FL_SPEC == 0 || PM_FL_SPEC == 2, "PM_FL_SPEC: 0 (product) or 2 (ablation)");
+// The FL kernels' text loads (ablation builds: -DPM_FL_TEXT_NT=1 loads the
+// text non-temporally, so its lines are the first out of L2)
+#if defined(PM_FL_TEXT_NT) && PM_FL_TEXT_NT
+#define PM_FL_TEXT_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define PM_FL_TEXT_LOAD(p) (*(p))
+#endif
 
 // A lane holds the records around its state: for a shallow record (granule
 // below GD, pm_flatten.h FlImage::deep_g) the 16-B half holding it, in
@@ -1643,7 +1650,7 @@ __device__ __forceinline__ bool fl_deep(uint32_t g, uint32_t GD) {
 
 template <int NR>
 __device__ __forceinline__ uint32_t fl_key(uint32_t g, bool deep) {
-    constexpr uint32_t DSHIFT = NR == 4 ? 3u : 2u;  // granules per deep block: 8 or 4
+    constexpr uint32_t DSHIFT = NR == 8 ? 4u : NR == 4 ? 3u : 2u;  // granules per deep block: 16, 8 or 4
     return deep ? (g >> DSHIFT) | 0x80000000u : g >> 1;
 }
 
@@ -1670,7 +1677,11 @@ __device__ __forceinline__ tu32x4 fl_reg(const FlHold<NR>& H, uint32_t g, bool d
     const uint32_t m2 = bmask(deep && (g & 2u));
     if (NR == 2) return bsel4(m2, H.R[0], H.R[NR - 1]);
     const uint32_t m4 = bmask(deep && (g & 4u));
-    return bsel4(m4, bsel4(m2, H.R[0], H.R[1 % NR]), bsel4(m2, H.R[2 % NR], H.R[3 % NR]));
+    const tu32x4 a = bsel4(m4, bsel4(m2, H.R[0], H.R[1 % NR]), bsel4(m2, H.R[2 % NR], H.R[3 % NR]));
+    if (NR == 4) return a;
+    const uint32_t m8 = bmask(deep && (g & 8u));  // NR 8: 128-B blocks
+    const tu32x4 b = bsel4(m4, bsel4(m2, H.R[4 % NR], H.R[5 % NR]), bsel4(m2, H.R[6 % NR], H.R[7 % NR]));
+    return bsel4(m8, a, b);
 }
 
 template <int KR, int NR>
@@ -1749,13 +1760,13 @@ __device__ __forceinline__ uint32_t fl_output(const uint8_t* __restrict__ base, 
 // instruction); 0: the count alone, no staging rows, no escapes, no stores.
 // NR: the 16-B halves a lane holds of a deep block (FlHold; each its own
 // instance, so profiles tell the picks' trials from the default's launches).
-template <int KR, int OUTW = 4, int NR = 2>
-__global__ __launch_bounds__(1024) void dfa_fl_kernel(
+template <int KR, int OUTW = 4, int NR = 2, int THREADS = 1024>
+__global__ __launch_bounds__(THREADS) void dfa_fl_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
     const uint16_t* __restrict__ rowout16, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
     static_assert(OUTW == 0 || OUTW == 2 || OUTW == 4, "u32 / u16 ids or the count");
-    constexpr int THREADS = 1024, BLK = 32, SROW = 17;
+    constexpr int BLK = 32, SROW = 17;
     constexpr bool kIds = OUTW != 0;
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
     __shared__ uint32_t s_ids[kIds ? THREADS * SROW : 1];
@@ -1800,7 +1811,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 for (int q = 0; q < 2; ++q) {
                     const tu32x4* tp = reinterpret_cast<const tu32x4*>(
                         tbase + ((uint32_t)lane * sl + (uint32_t)(BLK * (b0 + tt) + 16 * q)));
-                    const tu32x4 v = act[tt] ? *tp : tu32x4{0u, 0u, 0u, 0u};
+                    const tu32x4 v = act[tt] ? PM_FL_TEXT_LOAD(tp) : tu32x4{0u, 0u, 0u, 0u};
                     WT[tt][4 * q] = v.x;
                     WT[tt][4 * q + 1] = v.y;
                     WT[tt][4 * q + 2] = v.z;
@@ -1867,7 +1878,7 @@ __global__ __launch_bounds__(1024) void dfa_fl_kernel(
                 // every store's ids read first (one LDS wait per batch),
                 // inactive chains too; two batches where the lane holds 64-B
                 // blocks (registers)
-                constexpr int NBAT = NR == 4 ? 2 : 1, BST = NST / NBAT;
+                constexpr int NBAT = NR >= 4 ? 2 : 1, BST = NST / NBAT;
 #pragma unroll
                 for (int t0 = 0; t0 < NST; t0 += BST) {
                     tu32x4 vs[BST];
@@ -2093,7 +2104,7 @@ __global__ __launch_bounds__(1024) void dfa_fl2_kernel(
                 for (int q = 0; q < 2; ++q) {
                     const tu32x4* tp =
                         reinterpret_cast<const tu32x4*>(tb + ((uint32_t)lane * sl + (uint32_t)(BLK * b + 16 * q)));
-                    const tu32x4 v = act[k] ? *tp : tu32x4{0u, 0u, 0u, 0u};
+                    const tu32x4 v = act[k] ? PM_FL_TEXT_LOAD(tp) : tu32x4{0u, 0u, 0u, 0u};
                     WT[k][4 * q] = v.x;
                     WT[k][4 * q + 1] = v.y;
                     WT[k][4 * q + 2] = v.z;

@@ -994,12 +994,12 @@ void pm_hip_compile(void* obj) {
             FlImage fl;  // the fallback-linked form (pm_pack_sparse_fl)
             const std::vector<uint8_t> prof = pm_fl_profile(o->pats);  // the LDS rows' profile
             if (pm_pack_sparse_fl(im.dfa, fl, &prof)) {
-                fl.block.resize(fl.block.size() + 16, 0u);  // the last aligned 32-B block
+                fl.block.resize(fl.block.size() + 32, 0u);  // the last aligned 128-B block
                 o->dfa.flbase = (const uint8_t*)dalloc_copy(o, fl.block.data(), fl.block.size() * 4);
                 o->dfa.flrowout16 = (const uint16_t*)dalloc_copy(o, fl.rowout16.data(), fl.rowout16.size() * 2);
                 o->dfa.flF = fl.F;
                 o->dfa.flGD = fl.deep_g;
-                o->dfa.flwords = (uint32_t)(fl.block.size() - 16);
+                o->dfa.flwords = (uint32_t)(fl.block.size() - 32);
             }
         }
     }

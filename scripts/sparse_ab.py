@@ -57,10 +57,12 @@ for st in args.streams.split(","):
         counts = {}
         for r in range(args.rounds + 1):
             for k in ks:
-                kk, hold, chains = (k.split(":") + ["", ""])[:3]  # kernel[:fl_hold[:fl_chains]]
+                kk, hold, chains, lanes = (k.split(":") + ["", "", ""])[:4]  # kernel[:fl_hold[:fl_chains[:fl_lanes]]]
                 assert m.set_option("sparse_kernel", int(kk)) == 0
                 assert m.set_option("fl_hold", int(hold or 0)) == 0
                 assert m.set_option("fl_chains", int(chains or 1)) == 0
+                if lanes:  # (an ablation build's option)
+                    assert m.set_option("fl_lanes", int(lanes)) == 0
                 cnt.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)

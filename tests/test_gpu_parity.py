@@ -1193,11 +1193,11 @@ def test_auto_switches_to_the_dfa_on_dense_deep_matches():
         assert torch.equal(got, want)
     # RT first (measured: it spills), then two trial launches of each DFA
     # candidate (dense rows; rows + records with 16-B halves, two chains per
-    # lane, 32-B and 64-B record loads; the second of each timed); the
-    # fastest per position holds
-    assert kernels[:11] == [pm.KIND_RT] + [pm.KIND_AC] * 10, kernels
-    assert forms[:11] == [0, 1, 1] + [2] * 8, forms
-    assert len(set(zip(kernels[11:], forms[11:]))) == 1, (kernels, forms)
+    # lane, 64-B deep blocks; the second of each timed); the fastest per
+    # position holds
+    assert kernels[:9] == [pm.KIND_RT] + [pm.KIND_AC] * 8, kernels
+    assert forms[:9] == [0, 1, 1] + [2] * 6, forms
+    assert len(set(zip(kernels[9:], forms[9:]))) == 1, (kernels, forms)
 
 
 @pytest.mark.parametrize("cap", [1, 2])
@@ -1434,9 +1434,9 @@ def test_ac_kind_times_both_dfa_forms(stream):
         forms.append(ac.dfa_form_last)
         assert torch.equal(got, want)
     # dense rows, then rows + records with 16-B halves, the same with two
-    # chains per lane, 32-B and 64-B record loads: two launches each, then
+    # chains per lane, and with 64-B deep blocks: two launches each, then
     # the fastest holds
-    assert forms[:10] == [1, 1] + [2] * 8 and forms[10] == forms[11] == forms[12] in (1, 2), forms
+    assert forms[:8] == [1, 1] + [2] * 6 and forms[8] == forms[9] == forms[10] in (1, 2), forms
     ac.reset()  # a new stream: the forms are timed again
     ac.scan_device(dt.data_ptr(), 0, 0, n, got.data_ptr(), None, s.cuda_stream)
     torch.cuda.synchronize()
