@@ -400,9 +400,16 @@ def main():
     global HBM_PEAK_GBS
     HBM_PEAK_GBS = lib.pm_hip_hbm_peak_gbs()  # the one constant the CLI's CSV prices against too
 
-    # start-up, per rank: the dictionary's parse, then compile() -- the host
-    # flatten (or the shared image cache's read) and the upload of this
-    # rank's replica of the automaton to its GPU
+    # start-up, per rank: the device runtime's first allocation (lazy init,
+    # ~150 ms, paid once per process: without it the first compile's upload
+    # would carry it -- profiles/r06/startup/startup_probe.json), the
+    # dictionary's parse, then compile() -- the host flatten (or the shared
+    # image cache's read) and the upload of this rank's replica of the
+    # automaton to its GPU
+    t_i0 = time.perf_counter()
+    torch.empty(1, device="cuda").zero_()
+    torch.cuda.synchronize()
+    init_ms = (time.perf_counter() - t_i0) * 1e3
     t_s0 = time.perf_counter()
     d = pm.Dictionary([os.path.join(DATA, x) for x in DICTS[args.dict]])
     dict_ms = (time.perf_counter() - t_s0) * 1e3
@@ -413,7 +420,8 @@ def main():
     m.add_dictionary(d)
     compile_ordered(m.compile, cache_dir, use_dist, rank, dist)
     cs = m.compile_stats()
-    startup = {"dict_load_ms": round(dict_ms, 2), "compile_ms": cs["compile_ms"], "upload_ms": cs["upload_ms"],
+    startup = {"runtime_init_ms": round(init_ms, 2), "dict_load_ms": round(dict_ms, 2),
+               "compile_ms": cs["compile_ms"], "upload_ms": cs["upload_ms"],
                "image_bytes": cs["image_bytes"],
                "upload_gbps": round(cs["image_bytes"] / (cs["upload_ms"] * 1e-3) / 1e9, 2) if cs["upload_ms"] else None,
                "image_cache": ("hit" if cs["image_cache_hit"] else "miss") if cache_dir else "off",
