@@ -219,14 +219,20 @@ int pm_hip_set_device(int device);
  *   "fl_hold"         the fallback-linked kernel's record loads outside the
  *                     picks' trials: 2 = deep records' 32-B blocks (0, the
  *                     default), 4 = 64-B blocks, 1 = every record as a 16-B
- *                     half (the ac / auto picks time all three)
+ *                     half (the ac / auto picks time 1 and 4, and 1 with two
+ *                     chains per lane)
+ *   "fl_chains"       segments per lane of the fallback-linked kernel
+ *                     outside the picks' trials: 1 (0, the default) or 2
+ *                     (dfa_fl2_kernel; with fl_hold 1 or 2)
  *   "dfa_sync"        1 = DFA warm-ups start at the last synchronizing 3-gram
  *                     (default), 0 = max_len - 1 bytes back
  *   "rt_small_max"    reverse-trie launches of at most this many positions
  *                     run one thread per position (-1 = default 256 Ki,
  *                     0 = never)
  *   "spill_cap_chunks" the reverse-trie spill region per wave, 1,024-position
- *                     chunks (1..16; 0 = default 16)
+ *                     chunks (1..16; 0 = the default fill: 4 for the count,
+ *                     2 with ids -- a full region is resolved where the
+ *                     other waves' streaming hides it)
  *   "host_spin" / "host_gid16" / "host_events" / "host_pool"
  *                     read_block's host path (-1 = the environment's
  *                     default, 0 / 1; csrc/pm_plugin.hip HostOpts).

@@ -139,6 +139,9 @@ def test_bench_json_line_contract():
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["scaling"] == "weak" and d["unit"] == "GB/s" and d["dtype"] == "u8" and d["vs_baseline"] is None
     assert "workload" in d["config"]
+    su = d["per_rank"][0]["startup"]  # start-up per rank
+    assert su["compile_ms"] > 0 and su["upload_ms"] >= 0 and su["image_bytes"] > 0 and su["image_cache"] == "off"
+    assert su["runtime_init_ms"] >= 0 and su["dict_load_ms"] > 0
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
