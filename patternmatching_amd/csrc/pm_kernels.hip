@@ -1936,7 +1936,13 @@ __global__ __launch_bounds__(THREADS) void dfa_fl_kernel(
 // chain A, chain B at each part.  Twice the staging rows (2 x 17 dwords a
 // lane, 136 KiB) leave LDS for FL2_LDS_ROWS rows when ids are written; the
 // count keeps FL_COUNT_LDS_ROWS.
-constexpr int FL2_LDS_ROWS = 24;
+// (ablation builds: -DPM_FL2_THREADS=768 -- 1,536 chains per CU, 56 rows,
+// the registers for 64-B deep blocks)
+#ifndef PM_FL2_THREADS
+#define PM_FL2_THREADS 1024
+#endif
+constexpr int FL2_THREADS = PM_FL2_THREADS;
+constexpr int FL2_LDS_ROWS = FL2_THREADS == 1024 ? 24 : 56;
 
 struct FlPend {
     uint32_t s, c, fb, x, lw, r0, y, g;
@@ -2018,13 +2024,13 @@ __device__ __forceinline__ uint32_t fl_out_get(uint32_t F, uint32_t GD, uint32_t
 // dfa_fl_kernel with two chains per lane (the segments of chain k of lane l
 // in a wave: wave base + 64 k + l, so each chain set of a wave is 64
 // consecutive segments and its stores are dfa_fl_kernel's whole lines).
-template <int KR, int OUTW = 4, int NR = 1>
-__global__ __launch_bounds__(1024) void dfa_fl2_kernel(
+template <int KR, int OUTW = 4, int NR = 1, int THREADS = 1024>
+__global__ __launch_bounds__(THREADS) void dfa_fl2_kernel(
     const uint8_t* __restrict__ text, int64_t stream_start, int64_t pos0, int64_t n, void* __restrict__ out,
     unsigned long long* __restrict__ count, const uint8_t* __restrict__ base, uint32_t F, uint32_t GD,
     const uint16_t* __restrict__ rowout16, int64_t warm, int64_t seg_len, const uint32_t* __restrict__ gram3) {
     static_assert(OUTW == 0 || OUTW == 2 || OUTW == 4, "u32 / u16 ids or the count");
-    constexpr int THREADS = 1024, BLK = 32, SROW = 17, CH = 2;
+    constexpr int BLK = 32, SROW = 17, CH = 2;
     constexpr bool kIds = OUTW != 0;
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[KR * 256];
     __shared__ uint32_t s_ids[kIds ? CH * THREADS * SROW : 1];
@@ -2571,7 +2577,8 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     // blocks
     const bool fl2 = sk == PM_SK_FL && t.flchains == 2;  // dfa_fl2_kernel: two chains per lane
     const int64_t ch = !t.coded ? 1 : sparse ? (fl2 ? 2 : 1) : DFA_CHAINS;
-    const int lanes_cu = sparse ? SDFA_LANES_PER_CU : t.coded && outw == 0 ? DFA_COUNT_LANES_PER_CU : DFA_LANES_PER_CU;
+    const int lanes_cu = sparse ? (fl2 ? FL2_THREADS : SDFA_LANES_PER_CU)
+                                : t.coded && outw == 0 ? DFA_COUNT_LANES_PER_CU : DFA_LANES_PER_CU;
     const int64_t lanes = (int64_t)num_cu * lanes_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
     const int64_t short_seg = std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
@@ -2582,7 +2589,7 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     if (sparse) {
         // persistent workgroups (LDS staged once each), at most one lane per
         // segment and SDFA_LANES_PER_CU lanes per CU
-        const int wgt = sk == PM_SK_FL ? 1024 : DFA_LDS_THREADS;
+        const int wgt = sk == PM_SK_FL ? (fl2 ? FL2_THREADS : 1024) : DFA_LDS_THREADS;
         int64_t wg = (nseg + wgt * ch - 1) / (wgt * ch);
         const int64_t cap = lanes / wgt;
         if (wg > cap) wg = cap;
@@ -2601,12 +2608,16 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
     } while (0)
                 if (fl2) {  // two chains per lane (NR 1 or 2: the registers of two holds)
 #define PM_FL2_LAUNCH(KR_, W_, NR_)                                                                              \
-    hipLaunchKernelGGL((dfa_fl2_kernel<KR_, W_, NR_>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, \
+    hipLaunchKernelGGL((dfa_fl2_kernel<KR_, W_, NR_, FL2_THREADS>), gs, bs, 0, s, text, stream_start, pos0, n, out, count, \
                        t.flbase, t.flF, t.flGD, t.flrowout16, t.warm, seg, g3)
                     if (t.flhold == 1) {
                         if (outw == 4) PM_FL2_LAUNCH(FL2_LDS_ROWS, 4, 1);
                         else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 1);
                         else PM_FL2_LAUNCH(FL_COUNT_LDS_ROWS, 0, 1);
+                    } else if (FL2_THREADS < 1024 && t.flhold == 4) {
+                        if (outw == 4) PM_FL2_LAUNCH(FL2_LDS_ROWS, 4, 4);
+                        else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 4);
+                        else PM_FL2_LAUNCH(FL_COUNT_LDS_ROWS, 0, 4);
                     } else {
                         if (outw == 4) PM_FL2_LAUNCH(FL2_LDS_ROWS, 4, 2);
                         else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 2);
