@@ -1624,6 +1624,9 @@ __device__ __forceinline__ int64_t wave_uniform64(int64_t v) {
 #define PM_FL_SPEC 0
 #endif
 static_assert(PM_FL_SPEC == 0 || PM_FL_SPEC == 2, "PM_FL_SPEC: 0 (product) or 2 (ablation)");
+#ifndef PM_FL_COUNT_TB
+#define PM_FL_COUNT_TB 2
+#endif
 // The FL kernels' text loads (ablation builds: -DPM_FL_TEXT_NT=1 loads the
 // text non-temporally, so its lines are the first out of L2)
 #if defined(PM_FL_TEXT_NT) && PM_FL_TEXT_NT
@@ -1801,11 +1804,14 @@ __global__ __launch_bounds__(THREADS) void dfa_fl_kernel(
         uint32_t w = 0;  // the root, reached by no word
         for (int64_t i = wlo; i < lo; ++i) w = fl_step<KR, NR>(base, F, GD, s_rows, w, text[i], cb, H, own);
         const int64_t nblk = seg_len / BLK;
-        for (int64_t b0 = 0; b0 < nblk; b0 += 2) {  // two blocks' text per load
-            bool act[2];
-            uint32_t WT[2][8];
+        // two blocks' text per load (the count: PM_FL_COUNT_TB, an ablation
+        // switch: 4 = a lane's whole 128-B text line at once)
+        constexpr int TB = OUTW == 0 ? PM_FL_COUNT_TB : 2;
+        for (int64_t b0 = 0; b0 < nblk; b0 += TB) {
+            bool act[TB];
+            uint32_t WT[TB][8];
 #pragma unroll
-            for (int tt = 0; tt < 2; ++tt) {
+            for (int tt = 0; tt < TB; ++tt) {
                 act[tt] = lo + BLK * (b0 + tt) + BLK <= hi;
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
@@ -1819,9 +1825,9 @@ __global__ __launch_bounds__(THREADS) void dfa_fl_kernel(
                 }
             }
             if (!__ballot(act[0])) break;
-            unroll_for<0, 2>([&](auto tc) {
+            unroll_for<0, TB>([&](auto tc) {
                 constexpr int tt = decltype(tc)::value;
-                if (tt == 1 && !__ballot(act[1])) return;
+                if (tt > 0 && !__ballot(act[tt])) return;
                 const int64_t b = b0 + tt;
                 uint32_t em = 0;
 #pragma unroll
