@@ -1627,6 +1627,11 @@ static_assert(PM_FL_SPEC == 0 || PM_FL_SPEC == 2, "PM_FL_SPEC: 0 (product) or 2 
 #ifndef PM_FL_COUNT_TB
 #define PM_FL_COUNT_TB 2
 #endif
+// dfa_fl2_kernel's id staging: one ds_write_b32 per two positions (1) or
+// one ds_write_b16 per position (0)
+#ifndef PM_FL2_PACKED_STAGING
+#define PM_FL2_PACKED_STAGING 1
+#endif
 // The FL kernels' text loads (ablation builds: -DPM_FL_TEXT_NT=1 loads the
 // text non-temporally, so its lines are the first out of L2)
 #if defined(PM_FL_TEXT_NT) && PM_FL_TEXT_NT
@@ -2060,6 +2065,7 @@ __global__ __launch_bounds__(THREADS) void dfa_fl2_kernel(
     const int64_t nwaves = (int64_t)gridDim.x * (THREADS / 64);
     const uint32_t sl = (uint32_t)seg_len;
     uint32_t cnt = 0, cb[CH], own[CH], w[CH];
+    uint32_t held16[CH] = {0u, 0u};  // PM_FL2_PACKED_STAGING: the even position of a pair
     FlHold<NR> H[CH];
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
@@ -2150,7 +2156,16 @@ __global__ __launch_bounds__(THREADS) void dfa_fl2_kernel(
                             const bool esc = !rec && code == DFA_ESC;
                             const uint32_t id = rec ? own[k] : code;
                             if (kIds) {
-                                my[k][j - 1] = (uint16_t)(esc ? (w[k] & DFA_STATE_MASK) : id);
+                                const uint32_t v16 = esc ? (w[k] & DFA_STATE_MASK) : id;
+#if PM_FL2_PACKED_STAGING
+                                // two positions per staging write: position
+                                // j - 1 even (jj 1, 3) is held, odd (jj 2, 0)
+                                // writes the pair's dword
+                                if (jj & 1) held16[k] = v16;
+                                else reinterpret_cast<uint32_t*>(my[k])[(j - 1) >> 1] = held16[k] | v16 << 16;
+#else
+                                my[k][j - 1] = (uint16_t)v16;
+#endif
                                 em[k] |= esc ? 1u << (j - 1) : 0u;
                             }
                             cnt += act[k] && id != 0u;  // an escape is a nonzero id
@@ -2171,7 +2186,12 @@ __global__ __launch_bounds__(THREADS) void dfa_fl2_kernel(
                 bool esc;
                 const uint32_t id = fl_out_get<NR>(F, GD, w[k], H[k], esc);
                 if (kIds) {
+#if PM_FL2_PACKED_STAGING
+                    reinterpret_cast<uint32_t*>(my[k])[(BLK - 1) >> 1] =
+                        held16[k] | (esc ? (w[k] & DFA_STATE_MASK) : id) << 16;
+#else
                     my[k][BLK - 1] = (uint16_t)(esc ? (w[k] & DFA_STATE_MASK) : id);
+#endif
                     em[k] |= esc ? 1u << (BLK - 1) : 0u;
                 }
                 cnt += act[k] && id != 0u;
@@ -2621,9 +2641,11 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                         else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 1);
                         else PM_FL2_LAUNCH(FL_COUNT_LDS_ROWS, 0, 1);
                     } else if (FL2_THREADS < 1024 && t.flhold == 4) {
-                        if (outw == 4) PM_FL2_LAUNCH(FL2_LDS_ROWS, 4, 4);
-                        else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 4);
-                        else PM_FL2_LAUNCH(FL_COUNT_LDS_ROWS, 0, 4);
+                        if constexpr (FL2_THREADS < 1024) {  // (the registers for 64-B blocks)
+                            if (outw == 4) PM_FL2_LAUNCH(FL2_LDS_ROWS, 4, 4);
+                            else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 4);
+                            else PM_FL2_LAUNCH(FL_COUNT_LDS_ROWS, 0, 4);
+                        }
                     } else {
                         if (outw == 4) PM_FL2_LAUNCH(FL2_LDS_ROWS, 4, 2);
                         else if (outw == 2) PM_FL2_LAUNCH(FL2_LDS_ROWS, 2, 2);
