@@ -91,6 +91,7 @@ SIGNATURES = {
     "pm_hip_parent_gid": (ctypes.c_uint32, [c_vp, ctypes.c_uint32]),
     "pm_hip_set_image_cache": (None, [c_vp, ctypes.c_char_p]),
     "pm_hip_image_cache_hit": (ctypes.c_int, [c_vp]),
+    "pm_hip_serve_stats": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "pm_hip_compile_stats": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "pm_hip_pattern_counts_device": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, c_vp, c_vp]),
     "pm_hip_gen_stream_device": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,

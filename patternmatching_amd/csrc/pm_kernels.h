@@ -114,6 +114,31 @@ hipError_t pm_launch_score(const uint32_t* algo, const uint32_t* real, int64_t n
 // whose dense answers are real: the suffix chain of every answer.
 hipError_t pm_launch_pattern_counts(const uint32_t* real, int64_t n, const uint32_t* parent, uint32_t n_gids,
                                    unsigned long long* hist, int num_cu, hipStream_t s);
+// The resident small-call server (rt_serve_kernel): a grid that stays on the
+// device between read_block calls and takes each call from a request line
+// in host memory instead of a launch.  PmServeReq (one 64-B line) and the
+// done flags live in coherent (fine-grained) pinned host memory.  A call:
+// the host writes seq, the fields, then seq2 = seq; workgroup 0 polls the
+// line (one 64-B read over the link) and copies it to device memory for the
+// others; a workgroup takes a request when seq2 is new and equals seq, scans its share of [pos0, pos0 + n) (text and out are
+// pinned host buffers) and then writes seq's low 32 bits into done[its
+// index].  A workgroup exits when stop equals its grid's generation or when
+// no request came for idle_ticks of the 100 MHz real-time counter.
+struct alignas(64) PmServeReq {
+    uint64_t seq;   // written first ...
+    uint64_t stop;  // = the generation of a grid that is to exit
+    const uint8_t* text;
+    void* out;
+    int64_t stream_start, pos0;
+    uint64_t n_outw;  // n | out width (4: u32 gids, 2: u16) << 56
+    uint64_t seq2;  // ... and last
+};
+constexpr int RT_SERVE_THREADS = 1024;
+// Launch the server grid (`blocks` workgroups) on s: requests after `seen`
+// are its work; gen identifies it for stop.  done has `blocks` u32 flags.
+// fwd: 64 B of device memory (workgroup 0's copy of the request line).
+hipError_t pm_launch_rt_serve(PmServeReq* req, uint64_t* fwd, uint32_t* done, int blocks, uint64_t seen,
+                              uint64_t gen, int64_t idle_ticks, const RtDev& t, hipStream_t s);
 hipError_t pm_launch_gen(uint8_t* dst, uint64_t offset, uint64_t n, uint64_t seed, int mode, hipStream_t s);
 hipError_t pm_launch_gen_lines(uint8_t* dst, uint64_t n, const uint8_t* pats, const uint32_t* offs, uint32_t npats,
                                uint64_t seed, hipStream_t s);

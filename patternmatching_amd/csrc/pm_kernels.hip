@@ -1134,6 +1134,189 @@ __global__ __launch_bounds__(RT_SMALL_THREADS) void rt_small_kernel(const uint8_
     }
 }
 
+// The resident small-call server (pm_kernels.h PmServeReq): the grid stays
+// on the device between read_block calls, so a 100 KiB call (measure.c:77,
+// 284) costs the link's round trips instead of a launch and a stream
+// synchronization (~20 us of the ~35, profiles/r05/small_call/).
+// Workgroup 0's first wave polls the request line (lanes 0-7 read its
+// eight words: one 64-B read over the link; the host writes seq, the fields,
+// then seq2, and a line is read whole, so seq2 == seq > seen is a complete
+// new request) and forwards it to a 64-B line in device memory the other
+// workgroups poll the same way.  A workgroup's share of the positions is 64-aligned; its
+// text window -- the share plus the walk's look-back, RtDev::back + 1 bytes,
+// 8-B aligned -- is copied from the pinned staging into LDS, and each lane
+// walks its positions with rt_one from there.  The results go straight into
+// the pinned result buffer; once every lane's stores have completed
+// (s_waitcnt) and the barrier, the first lane writes seq's low 32 bits into
+// done[wg].
+// Coherence without fences: every access to host memory is an access at
+// its coherence point (system-scope relaxed atomics: the sc0 sc1 bits), so
+// nothing needs a cache invalidated or written back -- acquire / release
+// fences here invalidate or write back the whole L2 per wave, taking the
+// walk's tables out of L2 (measured: 74 us a 100 KiB call with them, against
+// 31 us for a launch per call).
+// Every exit is reached: a stop naming this grid's generation, or idle_ticks
+// (100 MHz) with no request.  Idle waves sleep between polls (s_sleep).
+constexpr int RT_SERVE_WIN = 16384;  // LDS bytes of a workgroup's text window
+constexpr int RT_SERVE_POLLERS = 4;  // waves of workgroup 0 polling the host's line
+#ifndef PM_SERVE_TRACE
+#define PM_SERVE_TRACE 0  // ablation build: s_memrealtime stamps of workgroups 0 and 1 per request
+#endif
+// a 64-bit value the compiler then knows is wave-uniform (every branch on
+// it scalar: the loop below has barriers, and a branch the compiler thinks
+// divergent around them is structurized into a loop the waves never leave)
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+    // (the builtin returns int: through uint32_t, or the low half sign-extends)
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+    return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ uint64_t lane64(uint64_t x, int l) {  // lane l's x, wave-uniform
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
+    return (uint64_t)hi << 32 | lo;
+}
+template <class T>
+__device__ __forceinline__ T sys_load(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <class T>
+__device__ __forceinline__ void sys_store(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <class T>
+__device__ __forceinline__ T dev_load(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void dev_store(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ __launch_bounds__(RT_SERVE_THREADS) void rt_serve_kernel(PmServeReq* req, uint64_t* fwd, uint32_t* done,
+                                                                    uint64_t seen, uint64_t gen, int64_t idle_ticks,
+                                                                    RtDev t) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[RT_SERVE_WIN];
+    __shared__ uint64_t s_w[8];  // the request line
+    __shared__ uint32_t s_state;  // this request: 0 polling, 1 found, 2 exit
+    const uint64_t* const rq = reinterpret_cast<const uint64_t*>(req);
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t G = gridDim.x, wg = blockIdx.x;
+    if (tid == 0) s_state = 0;
+    __syncthreads();
+    for (;;) {
+        if (wg == 0 ? wid < RT_SERVE_POLLERS : wid == 0) {
+            // Workgroup 0 polls the host's line with RT_SERVE_POLLERS waves
+            // a quarter of a link round trip apart (a request is seen ~3/4 of
+            // a round trip sooner than by one poller); the other workgroups
+            // poll workgroup 0's copy of it in device memory with one wave.
+            // One workgroup on the link: many pollers of one host line slow
+            // the host's own reads of the results (128 of them 5x).
+            for (int q = 0; q < wid; ++q) __builtin_amdgcn_s_sleep(24);  // (~0.6 us each)
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint64_t w = 0;
+            uint32_t found = 0, quit = 0;
+            const uint64_t* const src = wg == 0 ? rq : fwd;
+            for (;;) {
+                w = wg == 0 ? sys_load(src + (tid & 7)) : dev_load(src + (tid & 7));  // lanes 0-7: the line's words
+                const uint64_t s2 = lane64(w, 7);
+                if (s2 > seen && s2 == lane64(w, 0)) {
+                    found = 1;
+                    break;
+                }
+                if (lane64(w, 1) == gen || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)idle_ticks) {
+                    quit = 1;
+                    break;
+                }
+                if (wg == 0 && __builtin_amdgcn_readfirstlane(
+                                   __hip_atomic_load(&s_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+                    break;  // another poller has decided
+                __builtin_amdgcn_s_sleep(1);
+            }
+#if PM_SERVE_TRACE
+            if ((tid & 63) == 0 && wg < 2 && found)
+                sys_store(reinterpret_cast<uint64_t*>(done + G + 16) + 8 * wg, __builtin_amdgcn_s_memrealtime());
+#endif
+            if (found) {  // (more than one poller may find it: the same words)
+                const int lane = tid & 63;
+                if (lane < 8 && lane != 1) s_w[lane] = w;
+                if (wg == 0) {  // forward: the fields, then seq and seq2
+                    if (lane >= 2 && lane < 7) dev_store(fwd + lane, w);
+                    __builtin_amdgcn_s_waitcnt(0);
+                    if (lane == 0 || lane == 7) dev_store(fwd + lane, w);
+                }
+                if (lane == 0) __hip_atomic_exchange(&s_state, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (quit && (tid & 63) == 0) {
+                uint32_t zero = 0;
+                __hip_atomic_compare_exchange_strong(&s_state, &zero, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(s_state) == 2) {  // (uniform)
+            if (wg == 0 && tid == 1) dev_store(fwd + 1, gen);  // the others exit too
+            return;
+        }
+        __syncthreads();  // every thread has read s_state
+        if (tid == 0) s_state = 0;  // (the next poll starts after the barriers below)
+        const uint64_t v = rfl64(s_w[0]);
+        seen = v;
+        const uint8_t* const text = reinterpret_cast<const uint8_t*>(rfl64(s_w[2]));
+        void* const out = reinterpret_cast<void*>(rfl64(s_w[3]));
+        const int64_t ss = (int64_t)rfl64(s_w[4]), pos0 = (int64_t)rfl64(s_w[5]);
+        const uint64_t nw = rfl64(s_w[6]);
+        const int64_t n = (int64_t)(nw & ((1ull << 56) - 1));
+        const bool w4 = (nw >> 56) == 4;
+        const int64_t per = ((n + G - 1) / G + 63) & ~(int64_t)63;
+        const int64_t a = wg * per < n ? wg * per : n, b = a + per < n ? a + per : n;
+        if (a < b) {  // (uniform)
+            const int64_t back = (int64_t)t.back + 4;  // rt_one reads text[i-3] and one byte past a leaf
+            const int64_t lo = (pos0 + a - back > ss ? pos0 + a - back : ss) & ~(int64_t)7;
+            const int64_t hi = (pos0 + b + 7) & ~(int64_t)7;  // the staging has 16 zero bytes after the block
+            if (hi - lo <= RT_SERVE_WIN) {
+                for (int64_t k = 8 * tid; k < hi - lo; k += 8 * RT_SERVE_THREADS)
+                    *reinterpret_cast<uint64_t*>(win + k) = sys_load(reinterpret_cast<const uint64_t*>(text + lo + k));
+                __syncthreads();
+#if PM_SERVE_TRACE
+                if (tid == 0 && wg < 2)
+                    sys_store(reinterpret_cast<uint64_t*>(done + G + 16) + 8 * wg + 1, __builtin_amdgcn_s_memrealtime());
+#endif
+                for (int64_t k = a + tid; k < b; k += RT_SERVE_THREADS) {
+                    const uint32_t r = rt_one(win, t.t12, t, pos0 + k - lo, ss - lo);
+                    if (w4) reinterpret_cast<uint32_t*>(out)[k] = r;
+                    else reinterpret_cast<uint16_t*>(out)[k] = (uint16_t)r;
+                }
+            } else {  // a look-back longer than the window: straight from the pinned staging
+                for (int64_t k = a + tid; k < b; k += RT_SERVE_THREADS) {
+                    const uint32_t r = rt_one(text, t.t12, t, pos0 + k, ss);
+                    if (w4) reinterpret_cast<uint32_t*>(out)[k] = r;
+                    else reinterpret_cast<uint16_t*>(out)[k] = (uint16_t)r;
+                }
+            }
+        }
+        // The results are ordinary stores: L2 merges them into whole lines,
+        // which go over the link at the writeback (stores at the coherence
+        // point go as partial lines, and the host then reads them at a
+        // fraction of the rate).  Every wave's stores reach L2, then one
+        // release per workgroup writes L2 back before the flag.
+#if PM_SERVE_TRACE
+        if (tid == 0 && wg < 2)
+            sys_store(reinterpret_cast<uint64_t*>(done + G + 16) + 8 * wg + 2, __builtin_amdgcn_s_memrealtime());
+#endif
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+#if PM_SERVE_TRACE
+        if (tid == 0 && wg < 2)
+            sys_store(reinterpret_cast<uint64_t*>(done + G + 16) + 8 * wg + 3, __builtin_amdgcn_s_memrealtime());
+#endif
+        if (tid == 0) __hip_atomic_store(done + wg, (uint32_t)v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#if PM_SERVE_TRACE
+        if (tid == 0 && wg < 2)
+            sys_store(reinterpret_cast<uint64_t*>(done + G + 16) + 8 * wg + 4, __builtin_amdgcn_s_memrealtime());
+#endif
+    }
+}
+
 constexpr int DFA_THREADS = 256;
 
 template <int OUTW>
@@ -1881,7 +2064,7 @@ __global__ __launch_bounds__(THREADS) void dfa_fl_kernel(
                 constexpr int LPC = OUTW == 4 ? 8 : 4, CPI = 64 / LPC, NST = 64 / CPI;
                 const uint64_t am = __ballot(act[tt]);
                 uint32_t lds_off = ((uint32_t)(lane / LPC) * SROW + (OUTW == 4 ? 2u : 4u) * (lane % LPC)) * 4u;
-                uint32_t go = (uint32_t)(lane / LPC) * sl + (uint32_t)(16 / OUTW) * (lane % LPC);
+                uint32_t go = (uint32_t)(lane / LPC) * sl + (uint32_t)(16 / (OUTW ? OUTW : 4)) * (lane % LPC);
                 asm volatile("" : "+v"(lds_off), "+v"(go));
                 const uint64_t mine = am >> (lane / LPC);  // bit CPI * t: chain of store t active
                 const bool full = am == ~0ull;
@@ -2216,7 +2399,7 @@ __global__ __launch_bounds__(THREADS) void dfa_fl2_kernel(
             for (int k = 0; k < CH; ++k) {
                 const uint64_t am = __ballot(act[k]);
                 uint32_t lds_off = ((uint32_t)(lane / LPC) * SROW + (OUTW == 4 ? 2u : 4u) * (lane % LPC)) * 4u;
-                uint32_t go = (uint32_t)(lane / LPC) * sl + (uint32_t)(16 / OUTW) * (lane % LPC);
+                uint32_t go = (uint32_t)(lane / LPC) * sl + (uint32_t)(16 / (OUTW ? OUTW : 4)) * (lane % LPC);
                 asm volatile("" : "+v"(lds_off), "+v"(go));
                 const uint64_t mine = am >> (lane / LPC);
                 const bool full = am == ~0ull;
@@ -2541,6 +2724,14 @@ static hipError_t launch_rt_impl(bool floor, const uint8_t* text, int64_t stream
 hipError_t pm_launch_rt(const uint8_t* text, int64_t stream_start, int64_t pos0, int64_t n, void* out, int outw,
                         unsigned long long* count, const RtDev& t, int num_cu, hipStream_t s) {
     return launch_rt_impl(false, text, stream_start, pos0, n, out, outw, count, t, num_cu, s);
+}
+
+hipError_t pm_launch_rt_serve(PmServeReq* req, uint64_t* fwd, uint32_t* done, int blocks, uint64_t seen,
+                              uint64_t gen, int64_t idle_ticks, const RtDev& t, hipStream_t s) {
+    if (blocks <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rt_serve_kernel, dim3((unsigned)blocks), dim3(RT_SERVE_THREADS), 0, s, req, fwd, done, seen,
+                       gen, idle_ticks, t);
+    return hipGetLastError();
 }
 
 hipError_t pm_launch_rt_floor(const uint8_t* text, int64_t n, void* out, int outw, const RtDev& t, int num_cu,

@@ -160,6 +160,7 @@ struct PipeSlot {
     AutoPick pick;
     bool busy = false;
     bool staged = false;    // small block: results land in h_res, copied out by finish
+    bool served = false;    // ... by the object's resident server, in its own h_res
     bool timed = false;     // ev0 / ev1 bracket the launch (device seconds)
     int w = 4;              // bytes per result position in h_res / d_res
     size_t off = 0, m = 0;  // block = positions [off, off + m) of the call
@@ -185,8 +186,9 @@ struct StreamSpill {
 //                hipStreamSynchronize (PM_HOST_SPIN, default 0: no faster)
 //   host_gid16   small read_block_gid calls bring u16 gids over the link and
 //                widen them on the host when every gid < 65,536
-//                (PM_HOST_GID16, default 0: the link wait shrinks 3 us, the
-//                widening costs 5 us more than the copy)
+//                (PM_HOST_GID16; default 1 for calls the resident server
+//                takes, 0 for launched ones: there the link wait shrinks
+//                3 us and the widening cost 5 us more than the copy, round 4)
 //   host_events  small calls bracket their launch with timing events for
 //                pm_hip_device_seconds (PM_HOST_SMALL_EVENTS, default 0:
 //                the two events cost 7 us of a 43-us 100 KiB call,
@@ -198,8 +200,38 @@ struct StreamSpill {
 // (Measured and removed, round 5: small calls replayed from captured HIP
 // graphs -- 100 KiB gids 43.3 -> 51.2 us per call, a replayed zero-copy
 // launch + wait 24.0 -> 38.0 us; profiles/r05/small_call/.)
+//   host_serve   small read_block calls of an rt object (the one-thread-per-
+//                position walk's sizes, RtDev::small_max) go to its resident
+//                server grid (Server below) instead of a launch each
+//                (PM_HOST_SERVE, default 1)
 struct HostOpts {
-    int spin = -1, gid16 = -1, events = -1, pool = -1;
+    int spin = -1, gid16 = -1, events = -1, pool = -1, serve = -1;
+};
+
+// The resident small-call server of an rt object (pm_kernels.h PmServeReq,
+// rt_serve_kernel): the request line and the grid's done flags in coherent
+// pinned host memory, coherent staging and result buffers of its own, and
+// its own stream.  A call posts a request and
+// spins on the done flags; a grid that has exited (idle for
+// PM_HOST_SERVE_IDLE_US, default 2,000 us, or stopped) is launched again --
+// also in the middle of a wait, when the grid ended just as the request came
+// (it then redoes the request: the writes are the same).  serve_stop() asks
+// the grid to exit without waiting (before launches that want the whole
+// device); pm_hip_free and the process's exit wait for it.
+struct Server {
+    PmServeReq* req = nullptr;  // then, 64 B on, `blocks` u32 done flags
+    uint32_t* done = nullptr;
+    uint64_t* fwd = nullptr;    // device memory: workgroup 0's copy of the request line
+    uint8_t* h_stage = nullptr;
+    uint32_t* h_res = nullptr;
+    size_t cap = 0;  // positions
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;  // recorded after the grid: complete once it exited
+    int blocks = 0;
+    uint64_t seq = 0, gen = 0;
+    bool live = false;  // a grid was launched and not yet told to stop
+    uint64_t launches = 0, calls = 0;
+    int64_t idle_us = -1;  // option "serve_idle_us" (-1: PM_HOST_SERVE_IDLE_US, default 2,000)
 };
 struct PmHip {
     int kind_req = KIND_RT;
@@ -248,6 +280,7 @@ struct PmHip {
     // rt / dfa): the host path's, and the DFA form (0 = timed choice, 1 =
     // dense rows, 2 = sparse)
     HostOpts hopt;
+    Server srv;
     int dfa_form = 0;
     uint64_t untimed_calls = 0;  // read_block launches since reset without timing events
     int last_sparse_kernel = 0;  // PmSparseKernel of the last sparse-form launch (0: none yet)
@@ -583,6 +616,146 @@ void par_range(size_t n, size_t grain, const F& f) {
     for (auto& t : th) t.join();
 }
 
+// Servers with a grid that may still run: at the process's exit each is
+// told to stop and waited for (the handler is registered after the HIP
+// runtime's own, so it runs before them), so no grid outlives the process.
+std::mutex g_srv_m;
+std::vector<Server*> g_srv;
+void serve_exit_all() {
+    std::lock_guard<std::mutex> l(g_srv_m);
+    for (Server* v : g_srv) {
+        __atomic_store_n(&v->req->stop, v->gen, __ATOMIC_SEQ_CST);
+        (void)hipStreamSynchronize(v->s);
+    }
+    g_srv.clear();
+}
+
+bool serve_on(const PmHip* o) { return o->kind == KIND_RT && opt_or_env(o->hopt.serve, "PM_HOST_SERVE", 1); }
+
+// Ask the grid to exit (no wait).
+void serve_stop(PmHip* o) {
+    Server& v = o->srv;
+    if (!v.live) return;
+    __atomic_store_n(&v.req->stop, v.gen, __ATOMIC_SEQ_CST);
+    v.live = false;
+}
+
+void serve_free(PmHip* o) {
+    Server& v = o->srv;
+    if (!v.req) return;
+    const int64_t idle_us = v.idle_us;
+    serve_stop(o);
+    (void)hipStreamSynchronize(v.s);
+    {
+        std::lock_guard<std::mutex> l(g_srv_m);
+        g_srv.erase(std::remove(g_srv.begin(), g_srv.end(), &v), g_srv.end());
+    }
+    (void)hipHostFree(v.req);
+    (void)hipHostFree(v.h_stage);
+    (void)hipHostFree(v.h_res);
+    (void)hipFree(v.fwd);
+    (void)hipEventDestroy(v.ev);
+    (void)hipStreamDestroy(v.s);
+    v = Server();
+    v.idle_us = idle_us;
+}
+
+void serve_launch(PmHip* o, uint64_t seen) {
+    Server& v = o->srv;
+    ++v.gen;
+    static const int64_t env_idle = std::max(10, env_int("PM_HOST_SERVE_IDLE_US", 2000));
+    const int64_t idle_us = v.idle_us >= 0 ? v.idle_us : env_idle;
+    RtDev t = o->rt;
+    PM_CHECK(pm_launch_rt_serve(v.req, v.fwd, v.done, v.blocks, seen, v.gen, idle_us * 100, t, v.s));
+    PM_CHECK(hipEventRecord(v.ev, v.s));
+    v.live = true;
+    ++v.launches;
+}
+
+// The server's buffers (first call): staging for [context | block | 16 zero
+// bytes] of a block of up to PIPE_SMALL_POSITIONS positions, u32 results.
+void serve_ready(PmHip* o) {
+    Server& v = o->srv;
+    if (v.req) return;
+    v.blocks = std::max(1, o->num_cu / 4);
+    if (const char* e = std::getenv("PM_SERVE_BLOCKS")) v.blocks = std::max(1, std::min(o->num_cu, std::atoi(e)));
+    v.cap = PIPE_SMALL_POSITIONS;
+    const unsigned coh = hipHostMallocCoherent | hipHostMallocMapped;
+    // (+ 256 B after the flags: the ablation build's trace, PM_SERVE_TRACE)
+    PM_CHECK(hipHostMalloc(&v.req, 64 + sizeof(uint32_t) * (size_t)v.blocks + 64 + 256, coh));
+    std::memset(v.req, 0, 64 + sizeof(uint32_t) * (size_t)v.blocks + 64 + 256);
+    v.done = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(v.req) + 64);
+    // (staging and results in ordinary pinned memory: the grid reads and
+    // writes them at the coherence point anyway, and the host reads coherent
+    // memory at a third of the rate -- 400 KB of results 24.8 against 9.1 us)
+    PM_CHECK(hipHostMalloc(&v.h_stage, v.cap + o->max_len + 64, hipHostMallocDefault));
+    PM_CHECK(hipHostMalloc(&v.h_res, v.cap * sizeof(uint32_t), hipHostMallocDefault));
+    PM_CHECK(hipMalloc(&v.fwd, 64));
+    PM_CHECK(hipMemset(v.fwd, 0, 64));
+    PM_CHECK(hipStreamCreateWithFlags(&v.s, hipStreamNonBlocking));
+    PM_CHECK(hipEventCreateWithFlags(&v.ev, hipEventDisableTiming));
+    static const bool registered = [] { return std::atexit(serve_exit_all) == 0; }();
+    (void)registered;
+    std::lock_guard<std::mutex> l(g_srv_m);
+    g_srv.push_back(&v);
+}
+
+// Post the request: positions [pos0, pos0 + n) of the server's staging
+// (context back to stream_start), results of outw bytes into its h_res.
+void serve_post(PmHip* o, int64_t stream_start, int64_t pos0, int64_t n, int outw) {
+    Server& v = o->srv;
+    PmServeReq* r = v.req;
+    const uint64_t s = ++v.seq;
+    ++v.calls;
+    // seq, the fields, seq2 (x86 stores are seen in order; the device reads
+    // the line whole and takes it when seq2 == seq)
+    __atomic_store_n(&r->seq, s, __ATOMIC_SEQ_CST);
+    r->text = v.h_stage;
+    r->out = v.h_res;
+    r->stream_start = stream_start;
+    r->pos0 = pos0;
+    r->n_outw = (uint64_t)n | (uint64_t)outw << 56;
+    __atomic_store_n(&r->seq2, s, __ATOMIC_SEQ_CST);  // after the staging and the fields
+    // a grid that exited (idle) or was stopped: a new one, which takes s
+    if (!v.live || hipEventQuery(v.ev) == hipSuccess) serve_launch(o, s - 1);
+}
+
+// Wait for every workgroup's done flag of the last request.
+void serve_wait(PmHip* o) {
+    Server& v = o->srv;
+    const uint32_t want = (uint32_t)v.seq;
+    int w = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1;; ++spin) {
+        while (w < v.blocks && __atomic_load_n(&v.done[w], __ATOMIC_ACQUIRE) == want) ++w;
+        if (w == v.blocks) {
+#ifdef PM_SERVE_TRACE
+            const uint64_t* tr = reinterpret_cast<const uint64_t*>(v.done + v.blocks + 16);
+            std::fprintf(stderr, "serve trace (10 ns): wg0 detect->window %lld walk %lld waitcnt+bar %lld flag %lld | "
+                         "wg1 detect-wg0 %lld ->window %lld walk %lld bar %lld flag %lld | host %.2f us\n",
+                         (long long)(tr[1] - tr[0]), (long long)(tr[2] - tr[1]), (long long)(tr[3] - tr[2]),
+                         (long long)(tr[4] - tr[3]), (long long)(tr[8] - tr[0]), (long long)(tr[9] - tr[8]),
+                         (long long)(tr[10] - tr[9]), (long long)(tr[11] - tr[10]), (long long)(tr[12] - tr[11]),
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
+#endif
+            return;
+        }
+        if ((spin & 1023) == 0) {
+            const hipError_t e = hipEventQuery(v.ev);
+            if (e == hipSuccess) {  // the grid ended before it saw the request
+                serve_launch(o, v.seq - 1);
+            } else if (e != hipErrorNotReady) {
+                fatal("resident server grid", e);
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                std::fprintf(stderr, "pm_hip: resident server: no answer in 60 s (%d of %d workgroups done)\n", w,
+                             v.blocks);
+                std::exit(EXIT_FAILURE);
+            }
+        }
+    }
+}
+
 hipError_t launch_cand(PmHip* o, AutoPick& ap, int c, const uint8_t* text, int64_t stream_start, int64_t pos0,
                        int64_t n, void* out, int outw, unsigned long long* count, hipStream_t s, const RtDev& t) {
     ap.last = c == CAND_RT ? KIND_RT : KIND_AC;
@@ -783,10 +956,16 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
     if (g_hprof_on) g_hprof[4] += 1;
     const bool pool = o->hopt.pool != 0;  // (the pool's size: PM_HOST_POOL)
     const bool gid16 = opt_or_env(o->hopt.gid16, "PM_HOST_GID16", 0);
+    // (served calls: u16 gids over the link by default -- 100 KiB gids 29.0
+    // -> 25.4 us, the host pool's widening under the halved link time;
+    // profiles/r06/serve/)
+    const bool gid16_served = opt_or_env(o->hopt.gid16, "PM_HOST_GID16", 1);
     const bool events = opt_or_env(o->hopt.events, "PM_HOST_SMALL_EVENTS", 0);
     auto finish = [&](PipeSlot& q) {
         lap(1);
-        if (opt_or_env(o->hopt.spin, "PM_HOST_SPIN", 0)) {
+        if (q.served) {
+            serve_wait(o);
+        } else if (opt_or_env(o->hopt.spin, "PM_HOST_SPIN", 0)) {
             hipError_t e;
             while ((e = hipStreamQuery(q.stream)) == hipErrorNotReady) {}
             PM_CHECK(e);
@@ -800,8 +979,9 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             o->dev_seconds += ms * 1e-3;
         }
         const pm_pattern_id_t* map = o->id_of_gid.data();
+        const uint32_t* const hres = q.served ? o->srv.h_res : q.h_res;
         if (out_gid && q.staged && q.w == 2) {  // widen
-            const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
+            const uint16_t* g = reinterpret_cast<const uint16_t*>(hres);
             uint32_t* dst = out_gid + q.off;
             small_par(pool, q.m, [&](size_t lo, size_t hi) {
                 for (size_t j = lo; j < hi; ++j) dst[j] = g[j];
@@ -810,10 +990,10 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             pm_pattern_id_t* dst = out_ids + q.off;
             auto map_ids = [&](size_t lo, size_t hi) {
                 if (narrow) {
-                    const uint16_t* g = reinterpret_cast<const uint16_t*>(q.h_res);
+                    const uint16_t* g = reinterpret_cast<const uint16_t*>(hres);
                     for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
                 } else {
-                    const uint32_t* g = q.h_res;
+                    const uint32_t* g = hres;
                     for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
                 }
             };
@@ -821,7 +1001,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             else par_range(q.m, (size_t)1 << 18, map_ids);
         } else if (q.staged) {
             small_par(pool, q.m, [&](size_t lo, size_t hi) {
-                std::memcpy(out_gid + q.off + lo, q.h_res + lo, (hi - lo) * sizeof(uint32_t));
+                std::memcpy(out_gid + q.off + lo, hres + lo, (hi - lo) * sizeof(uint32_t));
             });
         }
         q.busy = false;
@@ -833,10 +1013,18 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         if (q.busy) finish(q);
         const size_t m = std::min(pipe, n - done);
         ensure_slot(o, q, m);
+        q.staged = m <= PIPE_SMALL_POSITIONS;
+        // small blocks of an rt object: the resident server (its own
+        // staging and results), unless the call is to be timed
+        q.served = q.staged && !events && host_zero_copy() == 3 && serve_on(o) &&
+                   (int64_t)m <= (o->rt.small_max >= 0 ? o->rt.small_max : RT_SMALL_MAX);
+        if (q.served) serve_ready(o);
+        if (!q.staged) serve_stop(o);  // large blocks want the whole device
+        uint8_t* const hstage = q.served ? o->srv.h_stage : q.h_stage;
         // context: the last `keep` bytes of (history | buf[0, done))
         const size_t h = std::min(keep, o->hist.avail() + done);
         const size_t ctx = (h + 15) & ~(size_t)15;  // new bytes start 16-aligned
-        uint8_t* st = q.h_stage + ctx - h;
+        uint8_t* st = hstage + ctx - h;
         if (done >= h) {
             std::memcpy(st, buf + done - h, h);
         } else {
@@ -844,13 +1032,12 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             o->hist.copy_last(st, from_hist);
             std::memcpy(st + from_hist, buf, done);
         }
-        q.staged = m <= PIPE_SMALL_POSITIONS;
         // small blocks, zero-copy (host_zero_copy()): the kernel reads the
         // pinned staging (2) / writes the pinned results (1) over the link
         const bool zc_in = q.staged && (host_zero_copy() & 2), zc_out = q.staged && (host_zero_copy() & 1);
         if (q.staged) {  // [context | bytes | 16 zero bytes] in one DMA from pinned memory
-            std::memcpy(q.h_stage + ctx, buf + done, m);
-            std::memset(q.h_stage + ctx + m, 0, 16);
+            std::memcpy(hstage + ctx, buf + done, m);
+            std::memset(hstage + ctx + m, 0, 16);
             lap(0);
             if (!zc_in) PM_CHECK(hipMemcpyAsync(q.d_stage, q.h_stage, ctx + m + 16, hipMemcpyHostToDevice, q.stream));
         } else {
@@ -859,9 +1046,20 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
             PM_CHECK(hipMemcpyAsync(q.d_stage + ctx, buf + done, m, hipMemcpyHostToDevice, q.stream));
             PM_CHECK(hipMemcpyAsync(q.d_stage + ctx + m, q.h_stage + ctx, 16, hipMemcpyHostToDevice, q.stream));
         }
-        q.w = narrow || (out_gid && q.staged && fits16 && gid16) ? 2 : 4;
+        q.w = narrow || (out_gid && q.staged && fits16 && (q.served ? gid16_served : gid16)) ? 2 : 4;
         q.timed = !q.staged || events;
         if (!q.timed) o->untimed_calls++;
+        if (q.served) {
+            serve_post(o, (int64_t)(ctx - h), (int64_t)ctx, (int64_t)m, q.w);
+            o->last_kernel = KIND_RT;
+            o->last_form = 0;
+            o->last_out_width = q.w;
+            q.busy = true;
+            q.off = done;
+            q.m = m;
+            done += m;
+            continue;
+        }
         if (q.timed) PM_CHECK(hipEventRecord(q.ev0, q.stream));
         const uint8_t* text = zc_in ? q.h_stage : q.d_stage;
         void* res = zc_out ? q.h_res : q.d_res;
@@ -931,6 +1129,7 @@ void pm_hip_compile(void* obj) {
     const auto tc0 = std::chrono::steady_clock::now();
     o->upload_s = 0.0;
     PM_CHECK(hipSetDevice(o->device));
+    serve_free(o);  // a server grid of an earlier compile reads the old tables
     o->gids = pm_assign_gids(o->pats);
     o->kind = o->kind_req;
     // flattened tables, through the on-disk image cache when configured
@@ -1086,6 +1285,7 @@ void pm_hip_reset(void* obj) {
 void pm_hip_free(void* obj) {
     PmHip* o = as(obj);
     (void)hipSetDevice(o->device);
+    serve_free(o);  // before the tables it reads
     for (void* p : o->allocs) (void)hipFree(p);
     if (o->spill) (void)hipFree(o->spill);
     for (StreamSpill& x : o->sspill) {
@@ -1135,6 +1335,7 @@ static int scan_device(void* obj, const uint8_t* d_text, int64_t stream_start, i
         return -4;
     }
     hipError_t e = hipSetDevice(o->device);
+    serve_stop(o);  // a device launch wants the whole device
     if (e == hipSuccess) {
         // a captured launch keeps the compile-time scratch (a graph owns the
         // pointers it was captured with: replays of graphs of one object run
@@ -1247,6 +1448,13 @@ int pm_hip_hold_choice(void* obj, int launches) {
 
 void pm_hip_set_image_cache(void* obj, const char* dir) { as(obj)->cache_dir = dir ? dir : ""; }
 
+int pm_hip_serve_stats(void* obj, uint64_t* launches, uint64_t* calls) {
+    const PmHip* o = as(obj);
+    if (launches) *launches = o->srv.launches;
+    if (calls) *calls = o->srv.calls;
+    return 0;
+}
+
 int pm_hip_image_cache_hit(void* obj) { return as(obj)->cache_hit ? 1 : 0; }
 
 int pm_hip_compile_stats(void* obj, double* compile_ms, double* upload_ms) {
@@ -1340,6 +1548,16 @@ int pm_hip_set_option(void* obj, const char* name, int64_t value) {
     if (k == "host_gid16") return flag(o->hopt.gid16);
     if (k == "host_events") return flag(o->hopt.events);
     if (k == "host_pool") return flag(o->hopt.pool);
+    if (k == "serve_idle_us") {  // the server grid's idle life (>= 10 us; -1 = the default)
+        if (value != -1 && (value < 10 || value > 10000000)) return -1;
+        o->srv.idle_us = value;
+        serve_stop(o);  // the next call launches a grid with it
+        return 0;
+    }
+    if (k == "host_serve") {
+        if (value == 0) serve_stop(o);
+        return flag(o->hopt.serve);
+    }
     return -1;
 }
 

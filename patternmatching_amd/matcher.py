@@ -147,6 +147,14 @@ class HipMatcher:
                 "image_bytes": int(self.lib.pm_hip_table_bytes(self.obj)),
                 "image_cache_hit": bool(self.lib.pm_hip_image_cache_hit(self.obj))}
 
+    def serve_stats(self):
+        """The resident small-call server of an rt object ("host_serve"):
+        {"launches": grids launched, "calls": requests served}
+        (pm_hip_serve_stats)."""
+        la, ca = ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.pm_hip_serve_stats(self.obj, ctypes.byref(la), ctypes.byref(ca))
+        return {"launches": la.value, "calls": ca.value}
+
     def set_image_cache(self, directory: str):
         self.lib.pm_hip_set_image_cache(self.obj, directory.encode())
 

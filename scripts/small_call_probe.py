@@ -16,6 +16,9 @@ microseconds per call (median of 300, snort, RT kind, ASCII):
                      _events: with the per-call timing events (host_events)
   read_block_ids     the same for pattern ids (read_block; ac kind too)
   host_copy_400k     memcpy of 400 KB pinned -> pageable on the host
+  read_block_gid_serve0/1  the whole call with a launch per call (0) or
+                     through the object's resident server grid (1, the
+                     default for rt objects), with the host path's breakdown
 Prints one JSON object."""
 import ctypes
 import json
@@ -128,6 +131,40 @@ def call_ids(mm):
                                          ids.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p)))
 
 
+# the resident server grid (host_serve) against a launch per call, and the
+# host path's breakdown of each (staging, enqueue, wait, result copy)
+for sv in (0, 1):
+    assert m.set_option("host_serve", sv) == 0
+    m.reset()
+    res[f"read_block_gid_serve{sv}_us"] = timeit(call)
+    m.reset()
+    res[f"read_block_ids_serve{sv}_us"] = timeit(call_ids(m))
+    m.reset()
+    lib.pm_hip_host_profile(1, None)
+    for _ in range(REPS):
+        call()
+    prof = (ctypes.c_double * 5)()
+    lib.pm_hip_host_profile(0, prof)
+    res[f"read_block_gid_serve{sv}_breakdown_us"] = {
+        k: round(prof[i] / max(prof[4], 1) * 1e6, 2) for i, k in enumerate(("stage", "enqueue", "wait", "copy"))}
+    res[f"read_block_gid_serve{sv}_GBps"] = round(N / res[f"read_block_gid_serve{sv}_us"] / 1e3, 3)
+for g16 in (1, 0):  # u16 gids over the link through the server
+    assert m.set_option("host_gid16", g16) == 0
+    m.reset()
+    res[f"read_block_gid_serve1_gid16_{g16}_us"] = timeit(call)
+m.set_option("host_gid16", -1)
+outs = []
+for sv in (0, 1):  # the same ids either way, calls carrying state
+    assert m.set_option("host_serve", sv) == 0
+    m.reset()
+    got = []
+    for _ in range(4):
+        call()
+        got.append(gids.copy())
+    outs.append(np.concatenate(got))
+assert np.array_equal(outs[0], outs[1])
+m.set_option("host_serve", -1)
+res["serve_stats"] = m.serve_stats()
 ac = pm.HipMatcher("ac")
 ac.add_dictionary(d)
 ac.compile()

@@ -1541,3 +1541,74 @@ def test_auto_read_block_over_deep_then_sparse_blocks():
     r = matcher("et", "ac")
     for k in range(0, len(text), 8 << 20):
         assert np.array_equal(a.read_block_codes(text[k:k + (8 << 20)]), r.read_block_codes(text[k:k + (8 << 20)])), k
+
+
+def test_resident_server_small_calls():
+    """Small read_block calls of an rt object go to its resident server grid
+    (rt_serve_kernel, the "host_serve" option; measure.c:77, 284 chunks):
+    gids and pattern ids equal one large call's and the launch-per-call
+    path's.  A grid that exits when idle ("serve_idle_us") is launched again
+    by the next call -- also when it ends while a call waits for it (idle
+    times about as long as the gaps between calls) -- a scan_device launch
+    between calls stops it, and free() waits for it."""
+    import time
+    torch = _torch()
+    m = fresh_matcher("snort", "rt")
+    sizes = [100 << 10] * 8 + [1, 17, 255 << 10, 5000, 3, 100 << 10]
+    text = np.tile(SHIP, 1 + sum(sizes) // len(SHIP))[:sum(sizes)]
+    offs = np.cumsum([0] + sizes)
+    pieces = list(zip(offs[:-1], offs[1:]))
+    m.reset()
+    whole = m.read_block_gids(text)  # > 256 Ki positions: the pipeline, not the server
+    m.reset()
+    whole_ids = m.read_block_id_array(text)
+    s0 = m.serve_stats()
+    m.reset()
+    assert np.array_equal(np.concatenate([m.read_block_gids(text[a:b]) for a, b in pieces]), whole)
+    m.reset()
+    assert np.array_equal(np.concatenate([m.read_block_id_array(text[a:b]) for a, b in pieces]), whole_ids)
+    s1 = m.serve_stats()
+    assert s1["calls"] - s0["calls"] == 2 * len(sizes) and s1["launches"] >= 1
+    assert m.set_option("host_serve", 0) == 0
+    m.reset()
+    assert np.array_equal(np.concatenate([m.read_block_gids(text[a:b]) for a, b in pieces]), whole)
+    assert m.serve_stats() == s1  # launches per call
+    assert m.set_option("host_serve", 1) == 0
+    assert m.set_option("serve_idle_us", 9) == -1
+    # idle exits between calls: every call launches a grid again
+    assert m.set_option("serve_idle_us", 50) == 0
+    m.reset()
+    parts = []
+    for a, b in pieces:
+        time.sleep(0.003)
+        parts.append(m.read_block_gids(text[a:b]))
+    assert np.array_equal(np.concatenate(parts), whole)
+    s2 = m.serve_stats()
+    assert s2["launches"] - s1["launches"] >= len(sizes) // 2
+    # gaps about the idle time: grids end around the requests
+    rng = np.random.default_rng(5)
+    for idle in (10, 40, 200):
+        assert m.set_option("serve_idle_us", idle) == 0
+        m.reset()
+        parts = []
+        for a, b in pieces:
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < rng.uniform(0, 2.5 * idle) * 1e-6:
+                pass
+            parts.append(m.read_block_gids(text[a:b]))
+        assert np.array_equal(np.concatenate(parts), whole), idle
+    # a scan_device launch between calls
+    assert m.set_option("serve_idle_us", -1) == 0
+    n = 1 << 20
+    dev = torch.from_numpy(np.concatenate([pm.gen_stream(n, 2, 0), np.zeros(64, np.uint8)])).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    m.reset()
+    parts = []
+    for k, (a, b) in enumerate(pieces):
+        parts.append(m.read_block_gids(text[a:b]))
+        if k % 3 == 0:
+            m.scan_device(dev.data_ptr(), 0, 0, n, out.data_ptr(), None, s)
+    torch.cuda.synchronize()
+    assert np.array_equal(np.concatenate(parts), whole)
+    m.free()
