@@ -239,7 +239,8 @@ int pm_hip_set_device(int device);
  *                     host_events (default off): small read_block calls
  *                     (<= 256 Ki positions) record timing events for
  *                     pm_hip_device_seconds; the CLI turns it on
- *   "host_serve"      rt objects: small read_block calls go to a resident
+ *   "host_serve"      rt objects, and auto objects while their pick holds
+ *                     the reverse trie: small read_block calls go to a resident
  *                     server grid polling a doorbell in host memory instead
  *                     of a launch per call (-1 = PM_HOST_SERVE, default 1;
  *                     0 = a launch per call).  Calls timed by host_events
@@ -248,7 +249,7 @@ int pm_hip_set_device(int device);
  *                     (-1 = PM_HOST_SERVE_IDLE_US, default 2,000; >= 10);
  *                     the next call launches it again */
 int pm_hip_set_option(void* obj, const char* name, int64_t value);
-/* The resident server of an rt object (the "host_serve" option): grids
+/* The resident server of an rt / auto object (the "host_serve" option): grids
  * launched and requests served since the object was made.  0. */
 int pm_hip_serve_stats(void* obj, uint64_t* launches, uint64_t* calls);
 /* The reverse-trie kernel's streaming floor on this GPU: the same chunk

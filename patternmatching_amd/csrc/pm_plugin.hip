@@ -200,7 +200,8 @@ struct StreamSpill {
 // (Measured and removed, round 5: small calls replayed from captured HIP
 // graphs -- 100 KiB gids 43.3 -> 51.2 us per call, a replayed zero-copy
 // launch + wait 24.0 -> 38.0 us; profiles/r05/small_call/.)
-//   host_serve   small read_block calls of an rt object (the one-thread-per-
+//   host_serve   small read_block calls of an rt object, or of an auto object
+//                while its pick holds the RT kernel (the one-thread-per-
 //                position walk's sizes, RtDev::small_max) go to its resident
 //                server grid (Server below) instead of a launch each
 //                (PM_HOST_SERVE, default 1)
@@ -208,7 +209,7 @@ struct HostOpts {
     int spin = -1, gid16 = -1, events = -1, pool = -1, serve = -1;
 };
 
-// The resident small-call server of an rt object (pm_kernels.h PmServeReq,
+// The resident small-call server of an rt / auto object (pm_kernels.h PmServeReq,
 // rt_serve_kernel): the request line and the grid's done flags in coherent
 // pinned host memory, coherent staging and result buffers of its own, and
 // its own stream.  A call posts a request and
@@ -630,7 +631,9 @@ void serve_exit_all() {
     g_srv.clear();
 }
 
-bool serve_on(const PmHip* o) { return o->kind == KIND_RT && opt_or_env(o->hopt.serve, "PM_HOST_SERVE", 1); }
+bool serve_on(const PmHip* o) {
+    return (o->kind == KIND_RT || o->kind == KIND_AUTO) && opt_or_env(o->hopt.serve, "PM_HOST_SERVE", 1);
+}
 
 // Ask the grid to exit (no wait).
 void serve_stop(PmHip* o) {
@@ -1014,10 +1017,22 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         const size_t m = std::min(pipe, n - done);
         ensure_slot(o, q, m);
         q.staged = m <= PIPE_SMALL_POSITIONS;
-        // small blocks of an rt object: the resident server (its own
+        // small blocks of an rt / auto object: the resident server (its own
         // staging and results), unless the call is to be timed
         q.served = q.staged && !events && host_zero_copy() == 3 && serve_on(o) &&
                    (int64_t)m <= (o->rt.small_max >= 0 ? o->rt.small_max : RT_SMALL_MAX);
+        if (q.served && o->kind == KIND_AUTO) {
+            // an auto object's calls are served while its pick holds the RT
+            // kernel; its measurements (an RT launch, the DFA trials) launch
+            init_pick(q.pick, o->kind, o->dfa.sbase != nullptr);
+            resolve_pick(o, q.pick);
+            q.served = q.pick.hold > 0 && q.pick.chosen == CAND_RT && !q.pick.timing && !q.pick.pending;
+            if (q.served) {
+                --q.pick.hold;
+                q.pick.last = KIND_RT;
+                q.pick.last_form = 0;
+            }
+        }
         if (q.served) serve_ready(o);
         if (!q.staged) serve_stop(o);  // large blocks want the whole device
         uint8_t* const hstage = q.served ? o->srv.h_stage : q.h_stage;

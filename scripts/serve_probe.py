@@ -21,7 +21,8 @@ import patternmatching_amd as pm  # noqa: E402
 N = int(os.environ.get("SERVE_PROBE_BYTES", 100 << 10))
 REPS = 300
 lib = pm.load()
-m = pm.HipMatcher("rt")
+KIND = os.environ.get("SERVE_PROBE_KIND", "rt")  # or "auto" (random ASCII: its pick holds RT)
+m = pm.HipMatcher(KIND)
 m.add_dictionary(pm.Dictionary([os.path.join(REPO, "tests", "golden", "data", "snort.dict")]))
 m.compile()
 part = np.ascontiguousarray(pm.gen_stream(N, 1, 0))
@@ -49,7 +50,7 @@ def timeit(fn):
     return round(statistics.median(t) * 1e6, 2)
 
 
-res = {"bytes": N, "reps": REPS, "serve_blocks_env": os.environ.get("PM_SERVE_BLOCKS")}
+res = {"bytes": N, "reps": REPS, "kind": KIND, "serve_blocks_env": os.environ.get("PM_SERVE_BLOCKS")}
 for sv in (0, 1, 0, 1):
     assert m.set_option("host_serve", sv) == 0
     for g16 in (0, 1):

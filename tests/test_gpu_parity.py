@@ -1543,9 +1543,11 @@ def test_auto_read_block_over_deep_then_sparse_blocks():
         assert np.array_equal(a.read_block_codes(text[k:k + (8 << 20)]), r.read_block_codes(text[k:k + (8 << 20)])), k
 
 
-def test_resident_server_small_calls():
-    """Small read_block calls of an rt object go to its resident server grid
-    (rt_serve_kernel, the "host_serve" option; measure.c:77, 284 chunks):
+@pytest.mark.parametrize("kind", ["rt", "auto"])
+def test_resident_server_small_calls(kind):
+    """Small read_block calls of an rt object -- and of an auto object while
+    its pick holds the reverse trie (shallow text) -- go to its resident
+    server grid (rt_serve_kernel, the "host_serve" option; measure.c:77, 284):
     gids and pattern ids equal one large call's and the launch-per-call
     path's.  A grid that exits when idle ("serve_idle_us") is launched again
     by the next call -- also when it ends while a call waits for it (idle
@@ -1553,9 +1555,12 @@ def test_resident_server_small_calls():
     between calls stops it, and free() waits for it."""
     import time
     torch = _torch()
-    m = fresh_matcher("snort", "rt")
+    m = fresh_matcher("snort", kind)
     sizes = [100 << 10] * 8 + [1, 17, 255 << 10, 5000, 3, 100 << 10]
-    text = np.tile(SHIP, 1 + sum(sizes) // len(SHIP))[:sum(sizes)]
+    if kind == "rt":
+        text = np.tile(SHIP, 1 + sum(sizes) // len(SHIP))[:sum(sizes)]
+    else:  # shallow: the auto pick holds RT
+        text = pm.gen_stream(sum(sizes), 9, 0)
     offs = np.cumsum([0] + sizes)
     pieces = list(zip(offs[:-1], offs[1:]))
     m.reset()
@@ -1568,7 +1573,10 @@ def test_resident_server_small_calls():
     m.reset()
     assert np.array_equal(np.concatenate([m.read_block_id_array(text[a:b]) for a, b in pieces]), whole_ids)
     s1 = m.serve_stats()
-    assert s1["calls"] - s0["calls"] == 2 * len(sizes) and s1["launches"] >= 1
+    if kind == "rt":
+        assert s1["calls"] - s0["calls"] == 2 * len(sizes) and s1["launches"] >= 1
+    else:  # the first call of each pass measures (a launch); the hold serves
+        assert s1["calls"] - s0["calls"] >= len(sizes) and s1["launches"] >= 1
     assert m.set_option("host_serve", 0) == 0
     m.reset()
     assert np.array_equal(np.concatenate([m.read_block_gids(text[a:b]) for a, b in pieces]), whole)
@@ -1584,7 +1592,7 @@ def test_resident_server_small_calls():
         parts.append(m.read_block_gids(text[a:b]))
     assert np.array_equal(np.concatenate(parts), whole)
     s2 = m.serve_stats()
-    assert s2["launches"] - s1["launches"] >= len(sizes) // 2
+    assert s2["launches"] - s1["launches"] >= len(sizes) // (2 if kind == "rt" else 4)
     # gaps about the idle time: grids end around the requests
     rng = np.random.default_rng(5)
     for idle in (10, 40, 200):
