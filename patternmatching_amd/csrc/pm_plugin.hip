@@ -233,6 +233,7 @@ struct Server {
     bool live = false;  // a grid was launched and not yet told to stop
     uint64_t launches = 0, calls = 0;
     int64_t idle_us = -1;  // option "serve_idle_us" (-1: PM_HOST_SERVE_IDLE_US, default 2,000)
+    bool failed = false;   // its buffers could not be made: the object's calls launch
 };
 struct PmHip {
     int kind_req = KIND_RT;
@@ -677,30 +678,44 @@ void serve_launch(PmHip* o, uint64_t seen) {
 
 // The server's buffers (first call): staging for [context | block | 16 zero
 // bytes] of a block of up to PIPE_SMALL_POSITIONS positions, u32 results.
-void serve_ready(PmHip* o) {
+bool serve_ready(PmHip* o) {
     Server& v = o->srv;
-    if (v.req) return;
+    if (v.req) return true;
+    if (v.failed) return false;
     v.blocks = std::max(1, o->num_cu / 4);
     if (const char* e = std::getenv("PM_SERVE_BLOCKS")) v.blocks = std::max(1, std::min(o->num_cu, std::atoi(e)));
     v.cap = PIPE_SMALL_POSITIONS;
     const unsigned coh = hipHostMallocCoherent | hipHostMallocMapped;
-    // (+ 256 B after the flags: the ablation build's trace, PM_SERVE_TRACE)
-    PM_CHECK(hipHostMalloc(&v.req, 64 + sizeof(uint32_t) * (size_t)v.blocks + 64 + 256, coh));
-    std::memset(v.req, 0, 64 + sizeof(uint32_t) * (size_t)v.blocks + 64 + 256);
-    v.done = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(v.req) + 64);
+    const size_t req_bytes = 64 + sizeof(uint32_t) * (size_t)v.blocks + 64 + 256;  // (+ the trace build's stamps)
     // (staging and results in ordinary pinned memory: the grid reads and
     // writes them at the coherence point anyway, and the host reads coherent
     // memory at a third of the rate -- 400 KB of results 24.8 against 9.1 us)
-    PM_CHECK(hipHostMalloc(&v.h_stage, v.cap + o->max_len + 64, hipHostMallocDefault));
-    PM_CHECK(hipHostMalloc(&v.h_res, v.cap * sizeof(uint32_t), hipHostMallocDefault));
-    PM_CHECK(hipMalloc(&v.fwd, 64));
-    PM_CHECK(hipMemset(v.fwd, 0, 64));
-    PM_CHECK(hipStreamCreateWithFlags(&v.s, hipStreamNonBlocking));
-    PM_CHECK(hipEventCreateWithFlags(&v.ev, hipEventDisableTiming));
+    bool ok = hipHostMalloc(&v.req, req_bytes, coh) == hipSuccess;
+    ok = ok && hipHostMalloc(&v.h_stage, v.cap + o->max_len + 64, hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipHostMalloc(&v.h_res, v.cap * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipMalloc(&v.fwd, 64) == hipSuccess && hipMemset(v.fwd, 0, 64) == hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&v.s, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&v.ev, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {  // no server for this object: its calls launch, as without one
+        (void)hipGetLastError();
+        if (v.req) (void)hipHostFree(v.req);
+        if (v.h_stage) (void)hipHostFree(v.h_stage);
+        if (v.h_res) (void)hipHostFree(v.h_res);
+        if (v.fwd) (void)hipFree(v.fwd);
+        if (v.s) (void)hipStreamDestroy(v.s);
+        const int64_t idle_us = v.idle_us;
+        v = Server();
+        v.idle_us = idle_us;
+        v.failed = true;
+        return false;
+    }
+    std::memset(v.req, 0, req_bytes);
+    v.done = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(v.req) + 64);
     static const bool registered = [] { return std::atexit(serve_exit_all) == 0; }();
     (void)registered;
     std::lock_guard<std::mutex> l(g_srv_m);
     g_srv.push_back(&v);
+    return true;
 }
 
 // Post the request: positions [pos0, pos0 + n) of the server's staging
@@ -1021,6 +1036,7 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         // staging and results), unless the call is to be timed
         q.served = q.staged && !events && host_zero_copy() == 3 && serve_on(o) &&
                    (int64_t)m <= (o->rt.small_max >= 0 ? o->rt.small_max : RT_SMALL_MAX);
+        if (q.served) q.served = serve_ready(o);
         if (q.served && o->kind == KIND_AUTO) {
             // an auto object's calls are served while its pick holds the RT
             // kernel; its measurements (an RT launch, the DFA trials) launch
@@ -1033,7 +1049,6 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
                 q.pick.last_form = 0;
             }
         }
-        if (q.served) serve_ready(o);
         if (!q.staged) serve_stop(o);  // large blocks want the whole device
         uint8_t* const hstage = q.served ? o->srv.h_stage : q.h_stage;
         // context: the last `keep` bytes of (history | buf[0, done))
