@@ -1620,3 +1620,29 @@ def test_resident_server_small_calls(kind):
     torch.cuda.synchronize()
     assert np.array_equal(np.concatenate(parts), whole)
     m.free()
+
+
+def test_resident_servers_of_two_objects_interleaved():
+    """Two rt objects in one process, each with its own resident server grid,
+    their small read_block calls interleaved (the reference's loop keeps
+    several slots; measure.c:324-332): each object's ids equal its own
+    large call's; freeing one leaves the other serving."""
+    a, b = fresh_matcher("snort", "rt"), fresh_matcher("et", "rt")
+    text = pm.gen_stream(24 * (100 << 10), 4, 0)
+    chunks = [(o, o + (100 << 10)) for o in range(0, len(text), 100 << 10)]
+    whole = {}
+    for m in (a, b):
+        m.reset()
+        whole[id(m)] = m.read_block_gids(text)
+        m.reset()
+    parts = {id(a): [], id(b): []}
+    for k, (lo, hi) in enumerate(chunks):
+        for m in ((a, b) if k % 2 else (b, a)):
+            parts[id(m)].append(m.read_block_gids(text[lo:hi]))
+    for m in (a, b):
+        assert np.array_equal(np.concatenate(parts[id(m)]), whole[id(m)])
+        assert m.serve_stats()["calls"] >= len(chunks)
+    a.free()
+    b.reset()
+    assert np.array_equal(np.concatenate([b.read_block_gids(text[lo:hi]) for lo, hi in chunks]), whole[id(b)])
+    b.free()
