@@ -744,16 +744,25 @@ void serve_wait(PmHip* o) {
     const uint32_t want = (uint32_t)v.seq;
     int w = 0;
     const auto t0 = std::chrono::steady_clock::now();
+#ifdef PM_SERVE_TRACE
+    // the first stamp of workgroup 0 (written when it sees the request): its arrival
+    static uint64_t last0 = 0;
+    const volatile uint64_t* tr0 = reinterpret_cast<const uint64_t*>(v.done + v.blocks + 16);
+    while (*tr0 == last0 && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(100)) {}
+    last0 = *tr0;
+    const double ack_us = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6;
+#endif
     for (uint64_t spin = 1;; ++spin) {
         while (w < v.blocks && __atomic_load_n(&v.done[w], __ATOMIC_ACQUIRE) == want) ++w;
         if (w == v.blocks) {
 #ifdef PM_SERVE_TRACE
             const uint64_t* tr = reinterpret_cast<const uint64_t*>(v.done + v.blocks + 16);
             std::fprintf(stderr, "serve trace (10 ns): wg0 detect->window %lld walk %lld waitcnt+bar %lld flag %lld | "
-                         "wg1 detect-wg0 %lld ->window %lld walk %lld bar %lld flag %lld | host %.2f us\n",
+                         "wg1 detect-wg0 %lld ->window %lld walk %lld bar %lld flag %lld | host: wg0's detect stamp "
+                         "seen %.2f us, last flag %.2f us\n",
                          (long long)(tr[1] - tr[0]), (long long)(tr[2] - tr[1]), (long long)(tr[3] - tr[2]),
                          (long long)(tr[4] - tr[3]), (long long)(tr[8] - tr[0]), (long long)(tr[9] - tr[8]),
-                         (long long)(tr[10] - tr[9]), (long long)(tr[11] - tr[10]), (long long)(tr[12] - tr[11]),
+                         (long long)(tr[10] - tr[9]), (long long)(tr[11] - tr[10]), (long long)(tr[12] - tr[11]), ack_us,
                          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
 #endif
             return;
