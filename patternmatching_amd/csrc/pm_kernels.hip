@@ -1237,15 +1237,18 @@ __global__ __launch_bounds__(RT_SERVE_THREADS) void rt_serve_kernel(PmServeReq* 
             if ((tid & 63) == 0 && wg < 2 && found)
                 sys_store(reinterpret_cast<uint64_t*>(done + G + 16) + 8 * wg, __builtin_amdgcn_s_memrealtime());
 #endif
-            if (found) {  // (more than one poller may find it: the same words)
+            if (found) {
                 const int lane = tid & 63;
-                if (lane < 8 && lane != 1) s_w[lane] = w;
-                if (wg == 0) {  // forward: the fields, then seq and seq2
-                    if (lane >= 2 && lane < 7) dev_store(fwd + lane, w);
-                    __builtin_amdgcn_s_waitcnt(0);
-                    if (lane == 0 || lane == 7) dev_store(fwd + lane, w);
+                uint32_t old = 1;
+                if (lane == 0) old = __hip_atomic_exchange(&s_state, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (__builtin_amdgcn_readfirstlane(old) != 1) {  // the first poller to find it (the others skip)
+                    if (lane < 8 && lane != 1) s_w[lane] = w;
+                    if (wg == 0) {  // forward: the fields, then seq and seq2
+                        if (lane >= 2 && lane < 7) dev_store(fwd + lane, w);
+                        __builtin_amdgcn_s_waitcnt(0);
+                        if (lane == 0 || lane == 7) dev_store(fwd + lane, w);
+                    }
                 }
-                if (lane == 0) __hip_atomic_exchange(&s_state, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else if (quit && (tid & 63) == 0) {
                 uint32_t zero = 0;
                 __hip_atomic_compare_exchange_strong(&s_state, &zero, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
