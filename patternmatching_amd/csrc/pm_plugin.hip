@@ -16,6 +16,7 @@
 // (util.h:37-39 FatalExit semantics).  There is no CPU fallback: without a
 // HIP device, create() fails loudly.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -37,6 +38,10 @@
 #include "pm_hoststep.h"
 #include "pm_kernels.h"
 #include "pm_streamgen.h"
+
+#ifndef PM_NT_IDS
+#define PM_NT_IDS 1  // read_block's id map with non-temporal stores (0: plain stores)
+#endif
 
 namespace {
 
@@ -1016,7 +1021,14 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
         } else if (!out_gid) {
             pm_pattern_id_t* dst = out_ids + q.off;
             auto map_ids = [&](size_t lo, size_t hi) {
-                if (narrow) {
+                if (narrow && PM_NT_IDS) {
+                    // non-temporal 8-B stores: no read for ownership of the
+                    // caller's lines (800 KB for a 100 KiB call)
+                    const uint16_t* g = reinterpret_cast<const uint16_t*>(hres);
+                    long long* d = reinterpret_cast<long long*>(dst);
+                    for (size_t j = lo; j < hi; ++j) _mm_stream_si64(d + j, (long long)(uintptr_t)map[g[j]]);
+                    _mm_sfence();
+                } else if (narrow) {
                     const uint16_t* g = reinterpret_cast<const uint16_t*>(hres);
                     for (size_t j = lo; j < hi; ++j) dst[j] = map[g[j]];
                 } else {
