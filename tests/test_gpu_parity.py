@@ -1646,3 +1646,25 @@ def test_resident_servers_of_two_objects_interleaved():
     b.reset()
     assert np.array_equal(np.concatenate([b.read_block_gids(text[lo:hi]) for lo, hi in chunks]), whole[id(b)])
     b.free()
+
+
+def test_resident_server_process_exit_without_free():
+    """A process that ends right after a served small call, its object never
+    freed, exits cleanly: the exit handler stops the live grid and waits
+    for it (no grid outlives its process)."""
+    import subprocess
+    import sys
+    import time
+    code = (
+        "import sys, numpy as np\n"
+        f"sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})\n"
+        "import patternmatching_amd as pm\n"
+        f"m = pm.HipMatcher('rt'); m.add_dictionary(pm.Dictionary([{os.path.join(DATA, 'snort.dict')!r}])); m.compile()\n"
+        "g = m.read_block_gids(pm.gen_stream(100 << 10, 3, 0))\n"
+        "assert m.serve_stats()['calls'] == 1, m.serve_stats()\n"
+        "print('served', int(np.count_nonzero(g)))\n")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "served" in r.stdout
+    assert time.time() - t0 < 90
