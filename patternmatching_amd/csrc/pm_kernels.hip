@@ -2754,6 +2754,9 @@ hipError_t pm_launch_rt_floor(const uint8_t* text, int64_t n, void* out, int out
 // lines than the caches hold.  The uncoded kernel (automata of 2^20 states
 // or more): one chain per lane.
 constexpr int DFA_LANES_PER_CU = 512, DFA_COUNT_LANES_PER_CU = 1024, DFA_CHAINS = 2, DFA_DENSE_BLK = 32;
+#ifndef PM_DFA_SMALL_SEG
+#define PM_DFA_SMALL_SEG 32  // shortest segment of a launch below 1 Mi positions (64: round 5)
+#endif
 // The sparse form: 1,024 lanes per CU (two 512-lane lock-step workgroups,
 // or one 1,024-lane staged workgroup), one chain per lane, 32-position
 // blocks (MEASUREMENTS.md §4, profiles/r03/sdfa_lanes_*.txt, sdfa_occupancy_sweep.txt:
@@ -2801,7 +2804,9 @@ hipError_t pm_launch_dfa(const uint8_t* text, int64_t stream_start, int64_t pos0
                                 : t.coded && outw == 0 ? DFA_COUNT_LANES_PER_CU : DFA_LANES_PER_CU;
     const int64_t lanes = (int64_t)num_cu * lanes_cu;
     int64_t seg = (n + lanes * ch - 1) / (lanes * ch);
-    const int64_t short_seg = std::min<int64_t>(512, std::max<int64_t>(64, n >> 16));
+    // (launches below 1 Mi positions -- read_block's 100 KiB calls -- take
+    // 32-position segments: twice the lanes, half the dependent steps each)
+    const int64_t short_seg = std::min<int64_t>(512, std::max<int64_t>(n < (1 << 20) ? PM_DFA_SMALL_SEG : 64, n >> 16));
     if (seg < short_seg) seg = short_seg;
     const int64_t align = sparse ? SDFA_BLK : t.coded && outw != 0 ? DFA_DENSE_BLK : 16;
     seg = (seg + align - 1) / align * align;
