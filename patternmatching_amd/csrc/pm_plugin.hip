@@ -1070,7 +1070,10 @@ void scan_host(PmHip* o, const uint8_t* buf, size_t n, uint32_t* out_gid, pm_pat
                 q.pick.last_form = 0;
             }
         }
-        if (!q.staged) serve_stop(o);  // large blocks want the whole device
+        // a launched block wants the device to itself: the grid exits (an
+        // auto object holding a DFA form on deep input: 126 against 95 us a
+        // 100 KiB call with the grid left resident, profiles/r06/serve/)
+        if (!q.served) serve_stop(o);
         uint8_t* const hstage = q.served ? o->srv.h_stage : q.h_stage;
         // context: the last `keep` bytes of (history | buf[0, done))
         const size_t h = std::min(keep, o->hist.avail() + done);

@@ -25,7 +25,11 @@ KIND = os.environ.get("SERVE_PROBE_KIND", "rt")  # or "auto" (random ASCII: its 
 m = pm.HipMatcher(KIND)
 m.add_dictionary(pm.Dictionary([os.path.join(REPO, "tests", "golden", "data", "snort.dict")]))
 m.compile()
-part = np.ascontiguousarray(pm.gen_stream(N, 1, 0))
+if os.environ.get("SERVE_PROBE_STREAM") == "lines":  # deep: the lines stream
+    part = np.empty(N, np.uint8)
+    m.lib.pm_gen_lines_host(m.obj, part.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), N, 1)
+else:
+    part = np.ascontiguousarray(pm.gen_stream(N, 1, 0))
 gids = np.empty(N, np.uint32)
 ids = np.empty(N, np.uint64)
 
@@ -50,7 +54,8 @@ def timeit(fn):
     return round(statistics.median(t) * 1e6, 2)
 
 
-res = {"bytes": N, "reps": REPS, "kind": KIND, "serve_blocks_env": os.environ.get("PM_SERVE_BLOCKS")}
+res = {"bytes": N, "reps": REPS, "kind": KIND, "stream": os.environ.get("SERVE_PROBE_STREAM", "ascii"),
+       "serve_blocks_env": os.environ.get("PM_SERVE_BLOCKS")}
 for sv in (0, 1, 0, 1):
     assert m.set_option("host_serve", sv) == 0
     for g16 in (0, 1):
