@@ -171,9 +171,26 @@ __device__ __forceinline__ uint32_t rt_deep(const uint8_t* __restrict__ text, co
         const uint32_t c = text[i - d];
         const uint32_t kind = rec_kind(R), first = R.x & 0xFFFFFFu;
         if (kind == RT_REC_LEAF_K) return R.y;
-        if (kind == RT_REC_CHAIN_K) {  // one step of the run: its first byte
-            if (c != (R.w >> 24)) return R.y;
-            node = first;
+        if (kind == RT_REC_CHAIN_K) {
+            // the run's leading bytes that match, in one step (pm_flatten.h
+            // RT_REC_CHAIN: b_k at byte 7 - k of w:z); bytes past the run or
+            // the stream are read at an in-range position and not counted
+            const uint32_t L = (R.x >> 24) & 63u;
+            const uint32_t lim = avail - d < (int64_t)L ? (uint32_t)(avail - d) : L;  // >= 1
+            uint64_t win = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t kk = (uint32_t)k < lim ? (uint32_t)k : lim - 1u;
+                win |= (uint64_t)text[i - d - kk] << (8 * (7 - k));
+            }
+            const uint64_t dif = win ^ ((uint64_t)R.w << 32 | R.z);
+            uint32_t m = dif ? (uint32_t)__builtin_clzll(dif) >> 3 : 8u;
+            m = m < lim ? m : lim;
+            if (m == 0) return R.y;
+            node = first + m - 1u;
+            d += m;
+            if (m < L) return t.rec[node].y;  // stopped inside the run
+            continue;
         } else if (kind == RT_REC_KIDS_K) {
             const uint32_t j = rec_kid_index(R, c);
             if (j == ((R.x >> 24) & 63u)) return R.y;
