@@ -186,10 +186,11 @@ __device__ __forceinline__ uint32_t rt_deep(const uint8_t* __restrict__ text, co
             const uint64_t dif = win ^ ((uint64_t)R.w << 32 | R.z);
             uint32_t m = dif ? (uint32_t)__builtin_clzll(dif) >> 3 : 8u;
             m = m < lim ? m : lim;
-            if (m == 0) return R.y;
+            // stopped inside the run: no pattern ends at its inner records,
+            // so the answer is this record's (as the chunk loop's rounds take it)
+            if (m < L) return R.y;
             node = first + m - 1u;
             d += m;
-            if (m < L) return t.rec[node].y;  // stopped inside the run
             continue;
         } else if (kind == RT_REC_KIDS_K) {
             const uint32_t j = rec_kid_index(R, c);
